@@ -1,0 +1,183 @@
+"""ctypes binding of include/grt_api.h (the C ABI of libgrt.so).
+
+The structures below mirror the C layout field for field.  Loading fails loudly when
+the HIP library has not been built: there is no CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "lib" / "libgrt.so"
+
+GRT_ABI_VERSION = 1
+GRT_MAX_OBJECTS = 8
+GRT_MAX_HITS = 16
+
+# enums (grt_api.h)
+GEOM_EUCLIDEAN, GEOM_SCHWARZSCHILD, GEOM_KERR, GEOM_KERR_BL = 0, 1, 2, 3
+TEX_BITMAP, TEX_CHECKER, TEX_BLACKBODY = 0, 1, 2
+OBJ_SPHERE, OBJ_DISC = 0, 1
+TEMP_CONSTANT, TEMP_KERR_LUT = 0, 1
+CLASS_ESCAPED, CLASS_CAPTURED, CLASS_HIT = 0, 1, 2
+STATUS_OK, ERR_MAX_STEPS, ERR_NO_CIRCULAR_ORBIT, ERR_BELOW_RISCO, ERR_NON_FINITE_RADIUS = 0, 1, 2, 3, 4
+FLAG_HIT_OVERFLOW = 0x80
+STOP_NONE, STOP_HORIZON, STOP_CELESTIAL, STOP_NAN, STOP_CLOSED_ORBIT = 0, 1, 2, 3, 4
+
+_d = C.c_double
+_pd = C.POINTER(C.c_double)
+
+
+class TextureDesc(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("_pad", C.c_int32), ("beaming_exponent", _d),
+        ("rgba", C.POINTER(C.c_uint8)), ("width", C.c_uint32), ("height", C.c_uint32),
+        ("checker_width", _d), ("checker_height", _d), ("c1", _d * 4), ("c2", _d * 4),
+    ]
+
+
+class ObjectDesc(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("temp_kind", C.c_int32), ("radius", _d), ("center", _d * 3),
+        ("temperature", _d), ("inner_radius", _d), ("outer_radius", _d),
+        ("temp_constant", _d), ("r_isco", _d), ("lut_r", _pd), ("lut_t", _pd),
+        ("lut_n", C.c_uint32), ("_pad2", C.c_uint32), ("texture", TextureDesc),
+    ]
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [
+        ("position", _d * 4), ("velocity", _d * 4), ("tetrad", (_d * 4) * 4), ("alpha", _d),
+        ("tan_half_alpha", _d), ("rows", C.c_int64), ("cols", C.c_int64),
+        ("spatial_signature", _d), ("spatial_handedness", _d), ("sin_theta", _d), ("cos_theta", _d),
+    ]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32), ("geometry", C.c_int32), ("radius", _d), ("a", _d),
+        ("horizon_epsilon", _d), ("max_steps", C.c_uint64), ("max_radius", _d), ("step_size", _d),
+        ("epsilon", _d), ("camera", CameraDesc), ("celestial", TextureDesc),
+        ("celestial_temperature", _d), ("n_objects", C.c_uint32), ("_pad", C.c_uint32),
+        ("objects", ObjectDesc * GRT_MAX_OBJECTS), ("bb_log_t", _pd), ("bb_xyz", _pd),
+        ("bb_n", C.c_uint32), ("_pad3", C.c_uint32), ("srgb_to_linear", _d * 256),
+        ("object_hit_opacity_threshold", _d),
+    ]
+
+
+class GlobalOpts(C.Structure):
+    _fields_ = [
+        ("width", C.c_int64), ("height", C.c_int64), ("step_size", _d), ("max_steps", C.c_uint64),
+        ("max_radius", _d), ("epsilon", _d), ("camera_position", _d * 3), ("phi", _d),
+        ("theta", _d), ("psi", _d), ("tone_mapping", C.c_int32), ("show_sampling_mask", C.c_int32),
+        ("sampling_mask_color", C.c_uint8 * 3), ("_pad", C.c_uint8 * 5),
+    ]
+
+
+class AdaptiveConfig(C.Structure):
+    _fields_ = [
+        ("enabled", C.c_int32), ("samples_per_axis", C.c_uint32),
+        ("luminance_contrast_threshold", _d), ("opacity_contrast_threshold", _d),
+        ("has_minimum_luminance", C.c_int32), ("exclude_background_contrast", C.c_int32),
+        ("minimum_luminance", _d), ("object_hit_opacity_threshold", _d),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("accepted_steps", C.c_uint64), ("attempts", C.c_uint64), ("rays", C.c_uint64),
+        ("hit_overflows", C.c_uint64), ("kernel_ms", _d),
+    ]
+
+
+class Offsets(C.Structure):
+    _fields_ = [
+        ("count", C.c_uint64), ("pixel_index", C.POINTER(C.c_uint32)), ("dx", _pd), ("dy", _pd),
+    ]
+
+
+class AuxOut(C.Structure):
+    _fields_ = [("xyza64", _pd), ("steps", C.POINTER(C.c_uint32)), ("stop_reason", C.POINTER(C.c_uint8))]
+
+
+class GrtError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """The loaded libgrt.so.  Raises if the HIP library is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise GrtError(
+            f"{LIB_PATH} not found: the HIP extension is not built "
+            "(run `python -c 'import __graft_entry__; __graft_entry__.build()'` or "
+            "`make -C gr_raytracer_amd/csrc`). There is no CPU fallback.")
+    L = C.CDLL(str(LIB_PATH))
+    vp, u32, u64, i32, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32, C.c_int64
+    sigs = {
+        "grt_last_error": (C.c_char_p, []),
+        "grt_device_count": (C.c_int, []),
+        "grt_default_global_opts": (None, [C.POINTER(GlobalOpts)]),
+        "grt_default_adaptive_config": (None, [C.POINTER(AdaptiveConfig)]),
+        "grt_host_scene_load": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(GlobalOpts), C.POINTER(vp)]),
+        "grt_host_scene_desc": (C.POINTER(SceneDesc), [vp]),
+        "grt_host_scene_adaptive": (None, [vp, C.POINTER(AdaptiveConfig)]),
+        "grt_host_scene_destroy": (C.c_int, [vp]),
+        "grt_camera_build": (C.c_int, [i32, _d, _d, _pd, _pd, _d, i64, i64, _d, _d, _d, C.POINTER(CameraDesc)]),
+        "grt_stationary_velocity": (C.c_int, [i32, _d, _d, _pd, _pd]),
+        "grt_zamo_velocity": (C.c_int, [i32, _d, _d, _pd, _pd]),
+        "grt_cartesian_to_spherical": (None, [_pd, _pd]),
+        "grt_cartesian_to_boyer_lindquist": (None, [_d, _pd, _pd]),
+        "grt_kerr_temperature_lut": (C.c_int, [_d, _d, _d, _d, u32, _pd, _pd, _pd]),
+        "grt_r_isco": (_d, [_d, _d]),
+        "grt_blackbody_lut": (C.c_int, [u32, _pd, _pd]),
+        "grt_blackbody_xyz": (None, [_d, _d, _pd]),
+        "grt_srgb_to_xyza": (None, [C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8, _pd]),
+        "grt_xyz_to_srgb8": (C.c_int, [_pd, C.c_size_t, i32, _d, C.POINTER(C.c_uint8)]),
+        "grt_scene_create": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(vp)]),
+        "grt_scene_destroy": (C.c_int, [vp]),
+        "grt_render_pixels": (C.c_int, [vp, C.c_int, u32, u32, u32, u32, C.POINTER(Offsets),
+                                        C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8),
+                                        C.POINTER(AuxOut), C.POINTER(Stats)]),
+        "grt_render_pixels_async": (C.c_int, [vp, C.c_int, vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp]),
+        "grt_render_section": (C.c_int, [vp, C.c_int, u32, u32, u32, u32, C.POINTER(AdaptiveConfig), _pd, _pd,
+                                         C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(Stats)]),
+        "grt_set_launch_config": (C.c_int, [C.c_int, C.c_int]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = [
+    "grt_last_error", "grt_device_count", "grt_default_global_opts", "grt_default_adaptive_config",
+    "grt_host_scene_load", "grt_host_scene_desc", "grt_host_scene_adaptive", "grt_host_scene_destroy",
+    "grt_camera_build", "grt_stationary_velocity", "grt_zamo_velocity", "grt_cartesian_to_spherical",
+    "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
+    "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_xyz_to_srgb8", "grt_scene_create", "grt_scene_destroy",
+    "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config",
+]
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().grt_last_error().decode(errors="replace")
+        raise GrtError(f"{what} failed ({rc}): {msg}")
+
+
+def dptr(arr) -> _pd:
+    return arr.ctypes.data_as(_pd)
+
+
+def ptr(arr, ctype):
+    return arr.ctypes.data_as(C.POINTER(ctype))

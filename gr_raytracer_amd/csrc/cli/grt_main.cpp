@@ -1,0 +1,179 @@
+// grt_main.cpp — `grt`, the command line of the MI355X build, flag-compatible with
+// the reference's clap CLI (src/cli/cli.rs:5-113, src/main.rs:21-178) for `render`:
+//
+//   grt [--width N] [--height N] [--step-size H] [--max-steps N] [--max-radius R]
+//       [--epsilon E] [--camera-position x,y,z] [--phi A] [--theta A] [--psi A]
+//       [--tone-mapping reinhard|global-linear] [--show-sampling-mask]
+//       [--sampling-mask-color r,g,b] --config-file scene.toml
+//       render [--filename out.png|out.hdr] [--from-row N] [--from-col N]
+//              [--to-row N] [--to-col N]
+//
+// Extra (not in the reference): --device N selects the GPU, --resource-root DIR
+// resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/grt_api.h"
+
+namespace grt_host {
+bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err);
+bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint32_t h, std::string& err);
+}
+
+static int usage(const char* msg) {
+  std::fprintf(stderr, "error: %s\nusage: grt [global options] --config-file FILE render [--filename F]\n", msg);
+  return 2;
+}
+
+static bool split_csv(const std::string& s, std::vector<double>& out) {
+  out.clear();
+  size_t p = 0;
+  while (p <= s.size()) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    std::string tok = s.substr(p, q - p);
+    char* end = nullptr;
+    double v = std::strtod(tok.c_str(), &end);
+    if (tok.empty() || *end) return false;
+    out.push_back(v);
+    p = q + 1;
+  }
+  return true;
+}
+
+int main(int argc, char** argv) {
+  auto t_start = std::chrono::steady_clock::now();
+  grt_global_opts opts;
+  grt_default_global_opts(&opts);
+  std::string config_file, action, filename = "render.png", resource_root, raw_out;
+  long from_row = -1, from_col = -1, to_row = -1, to_col = -1;
+  int device = 0;
+  std::vector<std::string> args(argv + 1, argv + argc);
+  for (size_t i = 0; i < args.size(); ++i) {
+    std::string a = args[i], val;
+    bool has_eq = false;
+    size_t eq = a.find('=');
+    if (a.rfind("--", 0) == 0 && eq != std::string::npos) {
+      val = a.substr(eq + 1);
+      a = a.substr(0, eq);
+      has_eq = true;
+    }
+    auto next = [&](std::string& v) -> bool {
+      if (has_eq) {
+        v = val;
+        return true;
+      }
+      if (i + 1 >= args.size()) return false;
+      v = args[++i];
+      return true;
+    };
+    std::string v;
+    if (a == "render") { action = a; continue; }
+    if (a == "render-ray" || a == "render-ray-at" || a == "blackbody" || a == "blackbody-spectrum")
+      return usage(("subcommand '" + a + "' is outside this build's hot-path scope").c_str());
+    if (a == "--show-sampling-mask") { opts.show_sampling_mask = 1; continue; }
+    if (!next(v)) return usage(("missing value for " + a).c_str());
+    std::vector<double> nums;
+    if (a == "--width") opts.width = std::atoll(v.c_str());
+    else if (a == "--height") opts.height = std::atoll(v.c_str());
+    else if (a == "--step-size") opts.step_size = std::atof(v.c_str());
+    else if (a == "--max-steps") opts.max_steps = std::strtoull(v.c_str(), nullptr, 10);
+    else if (a == "--max-radius") opts.max_radius = std::atof(v.c_str());
+    else if (a == "--epsilon") opts.epsilon = std::atof(v.c_str());
+    else if (a == "--phi") opts.phi = std::atof(v.c_str());
+    else if (a == "--theta") opts.theta = std::atof(v.c_str());
+    else if (a == "--psi") opts.psi = std::atof(v.c_str());
+    else if (a == "--camera-position") {
+      if (!split_csv(v, nums) || nums.size() != 3) return usage("Camera position must be a vector of length 3");
+      for (int k = 0; k < 3; ++k) opts.camera_position[k] = nums[k];
+    } else if (a == "--tone-mapping") {
+      if (v == "reinhard") opts.tone_mapping = 0;
+      else if (v == "global-linear") opts.tone_mapping = 1;
+      else return usage("tone mapping must be reinhard or global-linear");
+    } else if (a == "--sampling-mask-color") {
+      if (!split_csv(v, nums) || nums.size() != 3) return usage("invalid RGB color; expected R,G,B");
+      for (int k = 0; k < 3; ++k) {
+        if (nums[k] < 0 || nums[k] > 255 || nums[k] != std::floor(nums[k])) return usage("invalid RGB color");
+        opts.sampling_mask_color[k] = (uint8_t)nums[k];
+      }
+    } else if (a == "-c" || a == "--config-file") config_file = v;
+    else if (a == "--filename") filename = v;
+    else if (a == "--from-row") from_row = std::atol(v.c_str());
+    else if (a == "--from-col") from_col = std::atol(v.c_str());
+    else if (a == "--to-row") to_row = std::atol(v.c_str());
+    else if (a == "--to-col") to_col = std::atol(v.c_str());
+    else if (a == "--device") device = std::atoi(v.c_str());
+    else if (a == "--resource-root") resource_root = v;
+    else if (a == "--raw-out") raw_out = v;
+    else return usage(("unknown argument " + a).c_str());
+  }
+  if (action != "render") return usage("missing subcommand (render)");
+  if (config_file.empty()) return usage("Config file is required for this action");
+
+  grt_host_scene* hs = nullptr;
+  if (grt_host_scene_load(config_file.c_str(), resource_root.empty() ? nullptr : resource_root.c_str(), &opts, &hs)) {
+    std::fprintf(stderr, "Error: %s\n", grt_last_error());
+    return 1;
+  }
+  grt_adaptive_config ac;
+  grt_host_scene_adaptive(hs, &ac);
+  grt_scene* scene = nullptr;
+  if (grt_scene_create(grt_host_scene_desc(hs), &scene)) {
+    std::fprintf(stderr, "Error: %s\n", grt_last_error());
+    return 1;
+  }
+  uint32_t r0 = from_row < 0 ? 0 : (uint32_t)from_row, c0 = from_col < 0 ? 0 : (uint32_t)from_col;
+  uint32_t r1 = to_row < 0 ? (uint32_t)opts.height : (uint32_t)to_row;
+  uint32_t c1 = to_col < 0 ? (uint32_t)opts.width : (uint32_t)to_col;
+  uint32_t w = c1 - c0, h = r1 - r0;
+  std::vector<double> xyza((size_t)w * h * 4);
+  double mask[4];
+  const double* maskp = nullptr;
+  if (opts.show_sampling_mask) {
+    grt_srgb_to_xyza(opts.sampling_mask_color[0], opts.sampling_mask_color[1], opts.sampling_mask_color[2], 255, mask);
+    maskp = mask;
+  }
+  grt_stats st;
+  uint64_t nsel = 0;
+  if (grt_render_section(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st)) {
+    std::fprintf(stderr, "Error: %s\n", grt_last_error());
+    return 1;
+  }
+  std::fprintf(stderr, "[grt] %llu rays, %llu accepted steps, %llu attempts, %llu supersampled pixels, kernel %.1f ms "
+               "(%.3e steps/s)\n",
+               (unsigned long long)st.rays, (unsigned long long)st.accepted_steps, (unsigned long long)st.attempts,
+               (unsigned long long)nsel, st.kernel_ms, st.accepted_steps / (st.kernel_ms * 1e-3));
+  std::string err;
+  bool ok;
+  if (filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".hdr") == 0) {
+    std::vector<float> rgb((size_t)w * h * 3);
+    for (size_t i = 0; i < (size_t)w * h; ++i)
+      for (int k = 0; k < 3; ++k) rgb[3 * i + k] = (float)xyza[4 * i + k];
+    ok = grt_host::hdr_encode_rgb(filename, rgb.data(), w, h, err);
+  } else {
+    std::vector<uint8_t> rgb((size_t)w * h * 3);
+    grt_xyz_to_srgb8(xyza.data(), (size_t)w * h, opts.tone_mapping, 1.0, rgb.data());
+    ok = grt_host::png_encode_rgb(filename, rgb.data(), w, h, err);
+  }
+  if (!ok) {
+    std::fprintf(stderr, "Error: %s\n", err.c_str());
+    return 1;
+  }
+  if (!raw_out.empty()) {
+    FILE* f = std::fopen(raw_out.c_str(), "wb");
+    if (f) {
+      std::fwrite(xyza.data(), 8, xyza.size(), f);
+      std::fclose(f);
+    }
+  }
+  grt_scene_destroy(scene);
+  grt_host_scene_destroy(hs);
+  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+  std::fprintf(stderr, "saved image to %s\nElapsed time: %.3f s\n", filename.c_str(), secs);
+  return 0;
+}

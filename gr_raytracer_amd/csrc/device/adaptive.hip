@@ -1,0 +1,151 @@
+// adaptive.hip — device side of the reference's adaptive supersampling
+// (render_section_to_cie_buffer_supersampled, raytracer.rs:257-458).
+//
+//  * select_kernel: the 8-neighbour stencil of collect_pixels_to_supersample
+//    (:386-458), one lane per pixel, neighbours in the reference order, first
+//    trigger wins (should_supersample_pair :91-108).  The reference loop is serial
+//    but every pixel's decision depends only on the 1-spp buffer, so it is a pure
+//    data-parallel stencil.
+//  * offsets_kernel: stratified jitter (stratified_sample_offset :145-159, splitmix64
+//    mix64 :132-143), samples_per_axis^2 samples per selected pixel, stratum order.
+//  * average_kernel: the ordered sum of the valid sub-samples and the 1/valid scale
+//    (supersample :334-380).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/grt_api.h"
+#include "kernels.h"
+
+namespace grt {
+
+__device__ __forceinline__ bool pair_triggers(const double* p, int pc, const double* q, int qc,
+                                              const AdaptiveParams& a) {
+  if (pc != qc) return true;
+  if (a.exclude_background_contrast && pc == GRT_CLASS_ESCAPED) return false;
+  bool visible = fmax(p[1], q[1]) > a.min_lum;
+  double lc = fabs(p[1] - q[1]) / (p[1] + q[1] + 1e-4);
+  double oc = fabs(p[3] - q[3]);
+  return visible && (lc > a.luminance_contrast_threshold || oc > a.opacity_contrast_threshold);
+}
+
+__global__ void select_kernel(const double* __restrict__ xyza, const uint8_t* __restrict__ cls,
+                              AdaptiveParams a, uint8_t* __restrict__ flags) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t n = (uint64_t)a.w * a.h;
+  if (i >= n) return;
+  int row = (int)(i / a.w), col = (int)(i % a.w);
+  const int sh[8][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 1}, {1, -1}, {1, 0}, {1, 1}};
+  const double* p = xyza + 4 * i;
+  int pc = cls[i];
+  uint8_t f = 0;
+  for (int s = 0; s < 8; ++s) {
+    int nr = row + sh[s][0], nc = col + sh[s][1];
+    if (nr < 0 || nr >= (int)a.h || nc < 0 || nc >= (int)a.w) continue;
+    uint64_t j = (uint64_t)nr * a.w + nc;
+    if (pair_triggers(p, pc, xyza + 4 * j, cls[j], a)) {
+      f = 1;
+      break;
+    }
+  }
+  flags[i] = f;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ double hash_pixel_samples(int64_t row, int64_t col, uint64_t k) {
+  uint64_t z = mix64((uint64_t)row + mix64((uint64_t)col + mix64(k)));
+  return (double)(z >> 11) * (1.0 / (double)(1ull << 53));
+}
+
+__global__ void offsets_kernel(const uint32_t* __restrict__ sel, uint64_t n_sel, uint32_t spa,
+                               uint32_t row0, uint32_t col0, uint32_t w, uint32_t* __restrict__ pix,
+                               double* __restrict__ dx, double* __restrict__ dy) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t per = (uint64_t)spa * spa;
+  if (k >= n_sel * per) return;
+  uint64_t j = k / per, s = k % per;
+  uint32_t p = sel[j];
+  int64_t row = row0 + p / w, col = col0 + p % w;
+  uint64_t sr = s / spa, sc = s % spa;
+  uint64_t idx = sr * spa + sc;
+  pix[k] = p;
+  dx[k] = ((double)sc + hash_pixel_samples(row, col, 2 * idx)) / (double)spa;
+  dy[k] = ((double)sr + hash_pixel_samples(row, col, 2 * idx + 1)) / (double)spa;
+}
+
+__global__ void average_kernel(const uint32_t* __restrict__ sel, uint64_t n_sel, uint32_t spa,
+                               const double* __restrict__ samples, const uint8_t* __restrict__ status,
+                               double* __restrict__ out) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_sel) return;
+  uint64_t per = (uint64_t)spa * spa;
+  double x = 0.0, y = 0.0, z = 0.0, a = 0.0;
+  uint32_t valid = 0;
+  for (uint64_t s = 0; s < per; ++s) {
+    uint64_t k = j * per + s;
+    if ((status[k] & 0x7f) != GRT_OK) continue;
+    const double* c = samples + 4 * k;
+    x = x + c[0];
+    y = y + c[1];
+    z = z + c[2];
+    a = a + c[3];
+    valid++;
+  }
+  if (valid > 0) {
+    double inv = 1.0 / (double)valid;
+    double* o = out + 4 * (uint64_t)sel[j];
+    o[0] = x * inv;
+    o[1] = y * inv;
+    o[2] = z * inv;
+    o[3] = a * inv;
+  }
+}
+
+__global__ void paint_kernel(const uint32_t* __restrict__ sel, uint64_t n_sel, double m0, double m1,
+                             double m2, double m3, double* __restrict__ out) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_sel) return;
+  double* o = out + 4 * (uint64_t)sel[j];
+  o[0] = m0;
+  o[1] = m1;
+  o[2] = m2;
+  o[3] = m3;
+}
+
+static inline unsigned nblocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const AdaptiveParams& p,
+                         uint8_t* d_flags, hipStream_t stream) {
+  uint64_t n = (uint64_t)p.w * p.h;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(select_kernel, dim3(nblocks(n, 256)), dim3(256), 0, stream, d_xyza64, d_cls, p, d_flags);
+  return hipGetLastError();
+}
+hipError_t launch_make_offsets(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, uint32_t row0,
+                               uint32_t col0, uint32_t w, uint32_t* d_pix, double* d_dx, double* d_dy,
+                               hipStream_t stream) {
+  uint64_t n = n_sel * spa * spa;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(offsets_kernel, dim3(nblocks(n, 256)), dim3(256), 0, stream, d_sel, n_sel, spa, row0, col0, w,
+                     d_pix, d_dx, d_dy);
+  return hipGetLastError();
+}
+hipError_t launch_average(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, const double* d_samples,
+                          const uint8_t* d_status, double* d_out, hipStream_t stream) {
+  if (n_sel == 0) return hipSuccess;
+  hipLaunchKernelGGL(average_kernel, dim3(nblocks(n_sel, 256)), dim3(256), 0, stream, d_sel, n_sel, spa, d_samples,
+                     d_status, d_out);
+  return hipGetLastError();
+}
+hipError_t launch_paint(const uint32_t* d_sel, uint64_t n_sel, const double* mask, double* d_out,
+                        hipStream_t stream) {
+  if (n_sel == 0) return hipSuccess;
+  hipLaunchKernelGGL(paint_kernel, dim3(nblocks(n_sel, 256)), dim3(256), 0, stream, d_sel, n_sel, mask[0], mask[1],
+                     mask[2], mask[3], d_out);
+  return hipGetLastError();
+}
+
+}  // namespace grt

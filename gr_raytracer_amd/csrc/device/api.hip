@@ -1,0 +1,549 @@
+// api.hip — C ABI of the device hot path (include/grt_api.h).
+//
+// grt_scene_create deep-copies the caller's POD descriptor (textures and LUTs
+// included); each GPU receives its own device copy the first time it renders.
+// grt_render_pixels replaces Raytracer::render_section_to_cie_buffer_raw
+// (raytracer.rs:195-244) and supersample (:320-384); grt_render_section replaces
+// render_section_to_cie_buffer[_supersampled] (:177-318).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/grt_api.h"
+#include "../host/host_internal.h"
+#include "dev_scene.h"
+#include "kernels.h"
+
+namespace {
+
+int g_blocks_per_cu = 0;
+int g_threads = 256;
+
+int fail(int code, const std::string& msg) {
+  grt_host::set_error(msg);
+  return code;
+}
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      return fail(-EIO, std::string(#expr) + ": " + hipGetErrorString(_e));             \
+  } while (0)
+
+struct HostTexture {
+  std::vector<uint32_t> rgba;
+};
+
+struct DeviceCopy {
+  bool ready = false;
+  grt::DevScene* d_scene = nullptr;
+  std::vector<void*> allocations;
+  unsigned long long* d_counter = nullptr;  // [0] work counter
+  unsigned long long* d_stats = nullptr;    // [0..3] accepted, attempts, rays, overflows
+  int cus = 0;
+  int blocks = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::mutex mu;  // calls on one device are serialised
+};
+
+}  // namespace
+
+struct grt_scene {
+  grt_scene_desc desc;
+  HostTexture celestial;
+  HostTexture obj_tex[GRT_MAX_OBJECTS];
+  std::vector<double> lut_r[GRT_MAX_OBJECTS], lut_t[GRT_MAX_OBJECTS];
+  std::vector<double> bb_log_t, bb_xyz;
+  std::vector<DeviceCopy*> devices;
+};
+
+namespace {
+
+void copy_texture(const grt_texture_desc& t, HostTexture& out) {
+  if (t.kind == GRT_TEX_BITMAP && t.rgba && t.width && t.height) {
+    size_t n = (size_t)t.width * t.height;
+    out.rgba.resize(n);
+    std::memcpy(out.rgba.data(), t.rgba, n * 4);
+  }
+}
+
+template <class T>
+int upload(DeviceCopy& dc, const T* src, size_t n, T** dst) {
+  *dst = nullptr;
+  if (n == 0) return 0;
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, n * sizeof(T)));
+  dc.allocations.push_back(p);
+  HIP_TRY(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *dst = (T*)p;
+  return 0;
+}
+
+void fill_dev_texture(const grt_texture_desc& t, grt::DevTexture& d) {
+  d.kind = t.kind;
+  d.width = t.width;
+  d.height = t.height;
+  d.beaming = t.beaming_exponent;
+  d.rgba = nullptr;
+  d.cw = t.checker_width;
+  d.ch = t.checker_height;
+  for (int k = 0; k < 4; ++k) {
+    d.c1[k] = t.c1[k];
+    d.c2[k] = t.c2[k];
+  }
+}
+
+int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(-ENODEV, "invalid device ordinal");
+  if ((int)s->devices.size() < ndev) s->devices.resize(ndev, nullptr);
+  if (!s->devices[device]) s->devices[device] = new DeviceCopy();
+  DeviceCopy& dc = *s->devices[device];
+  *out = &dc;
+  if (dc.ready) return 0;
+  HIP_TRY(hipSetDevice(device));
+  const grt_scene_desc& d = s->desc;
+  grt::DevScene ds;
+  std::memset(&ds, 0, sizeof(ds));
+  ds.geometry = d.geometry;
+  ds.n_objects = d.n_objects;
+  ds.radius = d.radius;
+  ds.a = d.a;
+  ds.horizon_epsilon = d.horizon_epsilon;
+  // horizon thresholds exactly as schwarzschild.rs:181-183, kerr.rs:382-394, kerr_bl.rs:482-492
+  if (d.geometry == GRT_GEOM_SCHWARZSCHILD) {
+    ds.horizon_r = d.radius + d.horizon_epsilon;
+    ds.has_horizon = 1;
+  } else if (d.geometry == GRT_GEOM_KERR || d.geometry == GRT_GEOM_KERR_BL) {
+    double m = d.geometry == GRT_GEOM_KERR ? 0.5 * d.radius : d.radius / 2.0;
+    ds.has_horizon = !(std::fabs(d.a) > d.radius / 2.0);
+    double disc = std::fmax(m * m - d.a * d.a, 0.0);
+    double rp = m + std::sqrt(disc);
+    ds.horizon_r = rp + d.horizon_epsilon;
+  }
+  ds.max_steps = d.max_steps;
+  ds.max_radius_sq = d.max_radius * d.max_radius;
+  ds.step_size = d.step_size;
+  ds.epsilon = d.epsilon;
+  ds.trapped_radius = 5.0 * d.radius;
+  const grt_camera_desc& c = d.camera;
+  for (int k = 0; k < 4; ++k) {
+    ds.cam.pos[k] = c.position[k];
+    ds.cam.vel[k] = c.velocity[k];
+    for (int j = 0; j < 4; ++j) ds.cam.tet[k][j] = c.tetrad[k][j];
+  }
+  ds.cam.tan_half_alpha = c.tan_half_alpha;
+  ds.cam.rows = (double)c.rows;
+  ds.cam.cols = (double)c.cols;
+  ds.cam.sig_s = c.spatial_signature;
+  ds.cam.hand = c.spatial_handedness;
+  ds.cam.sin_theta = c.sin_theta;
+  ds.cam.cos_theta = c.cos_theta;
+  fill_dev_texture(d.celestial, ds.celestial);
+  ds.celestial_temperature = d.celestial_temperature;
+  ds.hit_threshold = d.object_hit_opacity_threshold;
+  ds.cos_half_pi = std::cos(1.57079632679489661923);
+  ds.sin_half_pi = std::sin(1.57079632679489661923);
+  int rc;
+  uint32_t* tex = nullptr;
+  if ((rc = upload(dc, s->celestial.rgba.data(), s->celestial.rgba.size(), &tex))) return rc;
+  ds.celestial.rgba = tex;
+  for (uint32_t k = 0; k < d.n_objects; ++k) {
+    const grt_object_desc& o = d.objects[k];
+    grt::DevObject& q = ds.obj[k];
+    q.kind = o.kind;
+    q.temp_kind = o.temp_kind;
+    q.radius = o.radius;
+    q.R2 = o.radius * o.radius;
+    q.cx = o.center[0];
+    q.cy = o.center[1];
+    q.cz = o.center[2];
+    q.temperature = o.temperature;
+    q.rin = o.inner_radius;
+    q.rout = o.outer_radius;
+    q.rin2 = o.inner_radius * o.inner_radius;
+    q.rout2 = o.outer_radius * o.outer_radius;
+    q.temp_constant = o.temp_constant;
+    q.r_isco = o.r_isco;
+    q.lut_n = o.lut_n;
+    double* lr = nullptr;
+    double* lt = nullptr;
+    if ((rc = upload(dc, s->lut_r[k].data(), s->lut_r[k].size(), &lr))) return rc;
+    if ((rc = upload(dc, s->lut_t[k].data(), s->lut_t[k].size(), &lt))) return rc;
+    q.lut_r = lr;
+    q.lut_t = lt;
+    fill_dev_texture(o.texture, q.tex);
+    uint32_t* ot = nullptr;
+    if ((rc = upload(dc, s->obj_tex[k].rgba.data(), s->obj_tex[k].rgba.size(), &ot))) return rc;
+    q.tex.rgba = ot;
+  }
+  double *bl = nullptr, *bx = nullptr, *sl = nullptr;
+  if ((rc = upload(dc, s->bb_log_t.data(), s->bb_log_t.size(), &bl))) return rc;
+  if ((rc = upload(dc, s->bb_xyz.data(), s->bb_xyz.size(), &bx))) return rc;
+  if ((rc = upload(dc, d.srgb_to_linear, 256, &sl))) return rc;
+  ds.bb_log_t = bl;
+  ds.bb_xyz = bx;
+  ds.bb_n = d.bb_n;
+  ds.srgb_lin = sl;
+  grt::DevScene* dsp = nullptr;
+  if ((rc = upload(dc, &ds, 1, &dsp))) return rc;
+  dc.d_scene = dsp;
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
+  dc.allocations.push_back(p);
+  dc.d_counter = (unsigned long long*)p;
+  dc.d_stats = dc.d_counter + 1;
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  dc.cus = prop.multiProcessorCount;
+  int occ = 0;
+  void (*kfn)() = nullptr;
+  (void)kfn;
+  int bpc = g_blocks_per_cu > 0 ? g_blocks_per_cu : 2;
+  dc.blocks = dc.cus * bpc;
+  HIP_TRY(hipEventCreate(&dc.ev0));
+  HIP_TRY(hipEventCreate(&dc.ev1));
+  (void)occ;
+  dc.ready = true;
+  return 0;
+}
+
+grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_t cols) {
+  grt::WorkList wl;
+  std::memset(&wl, 0, sizeof(wl));
+  wl.row0 = row0;
+  wl.col0 = col0;
+  wl.rows = rows;
+  wl.cols = cols;
+  wl.tiles_x = (cols + 7) / 8;
+  uint64_t tiles_y = (rows + 7) / 8;
+  wl.n_items = (uint64_t)wl.tiles_x * tiles_y * 64;
+  return wl;
+}
+
+// Enqueue one trace over `wl` on `stream`; counters are zeroed first.
+int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, const grt::Outputs& o,
+                  unsigned long long* d_stats, hipStream_t stream) {
+  HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
+  int threads = g_threads;
+  int blocks = g_blocks_per_cu > 0 ? dc.cus * g_blocks_per_cu : dc.blocks;
+  // never launch more lanes than there is work for
+  uint64_t max_blocks = (wl.n_items + threads - 1) / threads;
+  if ((uint64_t)blocks > max_blocks) blocks = (int)std::max<uint64_t>(1, max_blocks);
+  HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, o, dc.d_counter, d_stats, blocks, threads, stream));
+  return 0;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int alloc(size_t n) {
+    if (n == 0) n = 16;
+    HIP_TRY(hipMalloc(&p, n));
+    return 0;
+  }
+};
+
+int validate_desc(const grt_scene_desc* d) {
+  if (!d) return fail(-EINVAL, "null scene descriptor");
+  if (d->abi_version != GRT_ABI_VERSION) return fail(-EINVAL, "grt_scene_desc ABI version mismatch");
+  if (d->geometry < GRT_GEOM_EUCLIDEAN || d->geometry > GRT_GEOM_KERR_BL) return fail(-EINVAL, "unknown geometry");
+  if (d->n_objects > GRT_MAX_OBJECTS) return fail(-EINVAL, "too many objects");
+  auto check_tex = [&](const grt_texture_desc& t) -> int {
+    if (t.kind == GRT_TEX_BITMAP && (!t.rgba || !t.width || !t.height)) return fail(-EINVAL, "bitmap texture without texels");
+    if (t.kind == GRT_TEX_BLACKBODY && (d->bb_n < 2 || !d->bb_log_t || !d->bb_xyz))
+      return fail(-EINVAL, "blackbody texture without LUT");
+    if (t.kind < GRT_TEX_BITMAP || t.kind > GRT_TEX_BLACKBODY) return fail(-EINVAL, "unknown texture kind");
+    return 0;
+  };
+  int rc;
+  if ((rc = check_tex(d->celestial))) return rc;
+  for (uint32_t k = 0; k < d->n_objects; ++k) {
+    const grt_object_desc& o = d->objects[k];
+    if (o.kind != GRT_OBJ_SPHERE && o.kind != GRT_OBJ_DISC) return fail(-EINVAL, "unknown object kind");
+    if ((rc = check_tex(o.texture))) return rc;
+    if (o.kind == GRT_OBJ_DISC && o.temp_kind == GRT_TEMP_KERR_LUT && (o.lut_n < 2 || !o.lut_r || !o.lut_t))
+      return fail(-EINVAL, "disc temperature LUT missing");
+  }
+  if (d->camera.rows <= 0 || d->camera.cols <= 0) return fail(-EINVAL, "camera has no pixels");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int grt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int grt_set_launch_config(int blocks_per_cu, int threads_per_block) {
+  if (blocks_per_cu < 0 || threads_per_block < 0 || threads_per_block % 64 != 0 || threads_per_block > 256)
+    return fail(-EINVAL, "launch config: threads must be a multiple of 64 and <= 256");
+  g_blocks_per_cu = blocks_per_cu;
+  g_threads = threads_per_block ? threads_per_block : 256;
+  return 0;
+}
+
+int grt_scene_create(const grt_scene_desc* desc, grt_scene** out) {
+  if (!out) return fail(-EINVAL, "null output pointer");
+  int rc = validate_desc(desc);
+  if (rc) return rc;
+  grt_scene* s = new grt_scene();
+  s->desc = *desc;
+  copy_texture(desc->celestial, s->celestial);
+  for (uint32_t k = 0; k < desc->n_objects; ++k) {
+    const grt_object_desc& o = desc->objects[k];
+    copy_texture(o.texture, s->obj_tex[k]);
+    if (o.lut_n) {
+      s->lut_r[k].assign(o.lut_r, o.lut_r + o.lut_n);
+      s->lut_t[k].assign(o.lut_t, o.lut_t + o.lut_n);
+    }
+  }
+  if (desc->bb_n) {
+    s->bb_log_t.assign(desc->bb_log_t, desc->bb_log_t + desc->bb_n);
+    s->bb_xyz.assign(desc->bb_xyz, desc->bb_xyz + 3 * (size_t)desc->bb_n);
+  }
+  // the copy owns its arrays now
+  s->desc.celestial.rgba = nullptr;
+  for (uint32_t k = 0; k < desc->n_objects; ++k) {
+    s->desc.objects[k].texture.rgba = nullptr;
+    s->desc.objects[k].lut_r = nullptr;
+    s->desc.objects[k].lut_t = nullptr;
+  }
+  s->desc.bb_log_t = nullptr;
+  s->desc.bb_xyz = nullptr;
+  *out = s;
+  return 0;
+}
+
+int grt_scene_destroy(grt_scene* s) {
+  if (!s) return 0;
+  for (size_t dev = 0; dev < s->devices.size(); ++dev) {
+    DeviceCopy* dc = s->devices[dev];
+    if (!dc) continue;
+    (void)hipSetDevice((int)dev);
+    for (void* p : dc->allocations) (void)hipFree(p);
+    if (dc->ev0) (void)hipEventDestroy(dc->ev0);
+    if (dc->ev1) (void)hipEventDestroy(dc->ev1);
+    delete dc;
+  }
+  delete s;
+  return 0;
+}
+
+int grt_render_pixels_async(grt_scene* s, int device, void* stream, uint32_t row0, uint32_t col0,
+                            uint32_t rows, uint32_t cols, float* d_xyza, uint8_t* d_class,
+                            uint8_t* d_status, double* d_xyza64, uint32_t* d_steps, uint8_t* d_stop,
+                            uint64_t* d_stats) {
+  if (!s || !d_xyza || !d_class || !d_status || !d_stats) return fail(-EINVAL, "null argument");
+  if (rows == 0 || cols == 0) return 0;
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  grt::WorkList wl = rect_worklist(row0, col0, rows, cols);
+  grt::Outputs o{d_xyza, d_class, d_status, d_xyza64, d_steps, d_stop};
+  return enqueue_trace(s, *dc, wl, o, (unsigned long long*)d_stats, (hipStream_t)stream);
+}
+
+int grt_render_pixels(grt_scene* s, int device, uint32_t row0, uint32_t col0, uint32_t rows, uint32_t cols,
+                      const grt_offsets* offsets, float* xyza_out, uint8_t* class_out, uint8_t* status_out,
+                      const grt_aux_out* aux, grt_stats* stats) {
+  if (!s || !xyza_out || !class_out || !status_out) return fail(-EINVAL, "null argument");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  uint64_t n = offsets ? offsets->count : (uint64_t)rows * cols;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (n == 0) return 0;
+  grt::WorkList wl;
+  DevBuf b_pix, b_dx, b_dy;
+  if (offsets) {
+    if (!offsets->pixel_index || !offsets->dx || !offsets->dy) return fail(-EINVAL, "incomplete offsets");
+    if (cols == 0) return fail(-EINVAL, "offsets need the rectangle width");
+    for (uint64_t k = 0; k < n; ++k)
+      if (offsets->pixel_index[k] >= (uint64_t)rows * cols) return fail(-EINVAL, "offset pixel outside rectangle");
+    std::memset(&wl, 0, sizeof(wl));
+    wl.row0 = row0;
+    wl.col0 = col0;
+    wl.rows = rows;
+    wl.cols = cols;
+    wl.n_items = n;
+    if ((rc = b_pix.alloc(n * 4)) || (rc = b_dx.alloc(n * 8)) || (rc = b_dy.alloc(n * 8))) return rc;
+    HIP_TRY(hipMemcpy(b_pix.p, offsets->pixel_index, n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b_dx.p, offsets->dx, n * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b_dy.p, offsets->dy, n * 8, hipMemcpyHostToDevice));
+    wl.pixel_index = (const uint32_t*)b_pix.p;
+    wl.dx = (const double*)b_dx.p;
+    wl.dy = (const double*)b_dy.p;
+  } else {
+    wl = rect_worklist(row0, col0, rows, cols);
+  }
+  DevBuf b_xyza, b_cls, b_status, b_x64, b_steps, b_stop;
+  if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n))) return rc;
+  bool want64 = aux && aux->xyza64, want_steps = aux && aux->steps, want_stop = aux && aux->stop_reason;
+  if (want64 && (rc = b_x64.alloc(n * 32))) return rc;
+  if (want_steps && (rc = b_steps.alloc(n * 4))) return rc;
+  if (want_stop && (rc = b_stop.alloc(n))) return rc;
+  grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p,
+                 (uint32_t*)b_steps.p, (uint8_t*)b_stop.p};
+  hipStream_t st = nullptr;
+  HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(dc->ev0, st));
+  if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
+  HIP_TRY(hipEventRecord(dc->ev1, st));
+  HIP_TRY(hipEventSynchronize(dc->ev1));
+  HIP_TRY(hipMemcpy(xyza_out, b_xyza.p, n * 16, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
+  if (want64) HIP_TRY(hipMemcpy(aux->xyza64, b_x64.p, n * 32, hipMemcpyDeviceToHost));
+  if (want_steps) HIP_TRY(hipMemcpy(aux->steps, b_steps.p, n * 4, hipMemcpyDeviceToHost));
+  if (want_stop) HIP_TRY(hipMemcpy(aux->stop_reason, b_stop.p, n, hipMemcpyDeviceToHost));
+  if (stats) {
+    unsigned long long h[4];
+    HIP_TRY(hipMemcpy(h, dc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, dc->ev0, dc->ev1));
+    stats->accepted_steps = h[0];
+    stats->attempts = h[1];
+    stats->rays = h[2];
+    stats->hit_overflows = h[3];
+    stats->kernel_ms = ms;
+  }
+  return 0;
+}
+
+int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
+                       uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza,
+                       double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats) {
+  if (!s || !cfg || !xyza_out) return fail(-EINVAL, "null argument");
+  if (to_row < from_row || to_col < from_col) return fail(-EINVAL, "empty section");
+  if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  uint32_t w = to_col - from_col, h = to_row - from_row;
+  uint64_t n = (uint64_t)w * h;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (n_supersampled) *n_supersampled = 0;
+  if (n == 0) return 0;
+  hipStream_t st = nullptr;
+  DevBuf b_xyza, b_cls, b_status, b_x64;
+  if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n)) || (rc = b_x64.alloc(n * 32)))
+    return rc;
+  HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(dc->ev0, st));
+  grt::WorkList wl = rect_worklist(from_row, from_col, h, w);
+  grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p, nullptr, nullptr};
+  if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
+  bool supersampled = cfg->enabled || mask_xyza != nullptr;
+  uint64_t n_sel = 0;
+  if (supersampled) {
+    // resolve_minimum_luminance (raytracer.rs:118-129): exact 99th percentile in
+    // f64::total_cmp order, selected on the host from the device 1-spp buffer.
+    double min_lum = 0.0;
+    std::vector<double> x64(4 * n);
+    HIP_TRY(hipMemcpy(x64.data(), b_x64.p, n * 32, hipMemcpyDeviceToHost));
+    if (cfg->has_minimum_luminance) {
+      min_lum = cfg->minimum_luminance;
+    } else {
+      std::vector<double> lum(n);
+      for (uint64_t i = 0; i < n; ++i) lum[i] = x64[4 * i + 1];
+      uint64_t index = (uint64_t)((double)(n - 1) * 0.99);
+      auto key = [](double v) {
+        int64_t b;
+        std::memcpy(&b, &v, 8);
+        return b ^ (int64_t)((uint64_t)(b >> 63) >> 1);
+      };
+      std::nth_element(lum.begin(), lum.begin() + index, lum.end(),
+                       [&](double a, double b) { return key(a) < key(b); });
+      min_lum = 1e-3 * lum[index];
+    }
+    grt::AdaptiveParams ap;
+    ap.w = w;
+    ap.h = h;
+    ap.exclude_background_contrast = cfg->exclude_background_contrast;
+    ap.min_lum = min_lum;
+    ap.luminance_contrast_threshold = cfg->luminance_contrast_threshold;
+    ap.opacity_contrast_threshold = cfg->opacity_contrast_threshold;
+    DevBuf b_flags;
+    if ((rc = b_flags.alloc(n))) return rc;
+    HIP_TRY(grt::launch_select((const double*)b_x64.p, (const uint8_t*)b_cls.p, ap, (uint8_t*)b_flags.p, st));
+    std::vector<uint8_t> flags(n);
+    HIP_TRY(hipMemcpy(flags.data(), b_flags.p, n, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> sel;
+    for (uint64_t i = 0; i < n; ++i)
+      if (flags[i]) sel.push_back((uint32_t)i);
+    n_sel = sel.size();
+    if (n_sel) {
+      DevBuf b_sel;
+      if ((rc = b_sel.alloc(n_sel * 4))) return rc;
+      HIP_TRY(hipMemcpy(b_sel.p, sel.data(), n_sel * 4, hipMemcpyHostToDevice));
+      if (mask_xyza) {
+        HIP_TRY(grt::launch_paint((const uint32_t*)b_sel.p, n_sel, mask_xyza, (double*)b_x64.p, st));
+      } else {
+        uint32_t spa = cfg->samples_per_axis;
+        uint64_t ns = n_sel * spa * spa;
+        DevBuf b_pix, b_dx, b_dy, s_xyza, s_cls, s_status, s_x64;
+        if ((rc = b_pix.alloc(ns * 4)) || (rc = b_dx.alloc(ns * 8)) || (rc = b_dy.alloc(ns * 8)) ||
+            (rc = s_xyza.alloc(ns * 16)) || (rc = s_cls.alloc(ns)) || (rc = s_status.alloc(ns)) ||
+            (rc = s_x64.alloc(ns * 32)))
+          return rc;
+        HIP_TRY(grt::launch_make_offsets((const uint32_t*)b_sel.p, n_sel, spa, from_row, from_col, w,
+                                         (uint32_t*)b_pix.p, (double*)b_dx.p, (double*)b_dy.p, st));
+        grt::WorkList wo;
+        std::memset(&wo, 0, sizeof(wo));
+        wo.row0 = from_row;
+        wo.col0 = from_col;
+        wo.rows = h;
+        wo.cols = w;
+        wo.n_items = ns;
+        wo.pixel_index = (const uint32_t*)b_pix.p;
+        wo.dx = (const double*)b_dx.p;
+        wo.dy = (const double*)b_dy.p;
+        grt::Outputs so{(float*)s_xyza.p, (uint8_t*)s_cls.p, (uint8_t*)s_status.p, (double*)s_x64.p, nullptr, nullptr};
+        if ((rc = enqueue_trace(s, *dc, wo, so, dc->d_stats, st))) return rc;
+        HIP_TRY(grt::launch_average((const uint32_t*)b_sel.p, n_sel, spa, (const double*)s_x64.p,
+                                    (const uint8_t*)s_status.p, (double*)b_x64.p, st));
+        HIP_TRY(hipStreamSynchronize(st));
+      }
+    }
+  }
+  HIP_TRY(hipEventRecord(dc->ev1, st));
+  HIP_TRY(hipEventSynchronize(dc->ev1));
+  HIP_TRY(hipMemcpy(xyza_out, b_x64.p, n * 32, hipMemcpyDeviceToHost));
+  if (class_out) HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
+  if (n_supersampled) *n_supersampled = n_sel;
+  if (stats) {
+    unsigned long long hs[4];
+    HIP_TRY(hipMemcpy(hs, dc->d_stats, sizeof(hs), hipMemcpyDeviceToHost));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, dc->ev0, dc->ev1));
+    stats->accepted_steps = hs[0];
+    stats->attempts = hs[1];
+    stats->rays = hs[2];
+    stats->hit_overflows = hs[3];
+    stats->kernel_ms = ms;
+  }
+  return 0;
+}
+
+}  // extern "C"

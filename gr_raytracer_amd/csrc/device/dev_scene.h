@@ -1,0 +1,91 @@
+// dev_scene.h — device-resident scene layout for the gfx950 geodesic kernels.
+//
+// Built once per frame (per GPU) from grt_scene_desc by api.hip.  Every field is
+// read wave-uniformly, so the compiler serves it from the scalar cache (s_load);
+// textures and LUTs live in HBM behind plain pointers.
+#pragma once
+#include <stdint.h>
+
+namespace grt {
+
+struct DevTexture {
+  int32_t kind;  // grt_texture_kind
+  uint32_t width, height;
+  uint32_t _pad;
+  double beaming;
+  const uint32_t* rgba;  // RGBA8 texels, row-major
+  double cw, ch;         // checker cell counts
+  double c1[4], c2[4];   // checker colours, XYZA
+};
+
+struct DevObject {
+  int32_t kind;       // grt_object_kind
+  int32_t temp_kind;  // grt_temperature_kind
+  double radius, R2;  // sphere radius and radius.powi(2)
+  double cx, cy, cz;  // sphere centre
+  double temperature; // sphere constant temperature
+  double rin, rout, rin2, rout2;  // disc annulus
+  double temp_constant, r_isco;
+  const double* lut_r;
+  const double* lut_t;
+  uint32_t lut_n;
+  uint32_t _pad;
+  DevTexture tex;
+};
+
+struct DevCamera {
+  double pos[4];
+  double vel[4];
+  double tet[4][4];  // rows e_t, e_x, e_y, e_z
+  double tan_half_alpha;
+  double rows, cols;  // as f64 (camera.rs uses `as f64`)
+  double sig_s;       // spatial signature
+  double hand;        // spatial handedness
+  double sin_theta, cos_theta;  // of pos[2], host libm
+};
+
+struct DevScene {
+  int32_t geometry;
+  uint32_t n_objects;
+  double radius, a, horizon_epsilon;
+  // horizon test thresholds, evaluated on the host exactly as the reference does
+  double horizon_r;     // Schwarzschild: radius + eps; Kerr/KerrBL: r_plus + eps
+  int32_t has_horizon;  // Kerr/KerrBL: |a| <= M
+  int32_t _pad0;
+  uint64_t max_steps;
+  double max_radius_sq, step_size, epsilon;
+  double trapped_radius;  // TRAPPED_ORBIT_RADIUS_FACTOR * radius
+  DevCamera cam;
+  DevTexture celestial;
+  double celestial_temperature;
+  double hit_threshold;   // object_hit_opacity_threshold
+  double cos_half_pi, sin_half_pi;  // host libm cos(pi/2), sin(pi/2)
+  const double* bb_log_t;
+  const double* bb_xyz;
+  uint32_t bb_n;
+  uint32_t _pad1;
+  const double* srgb_lin;  // 256 entries
+  DevObject obj[8];
+};
+
+// Work description for one launch.
+struct WorkList {
+  uint32_t row0, col0, rows, cols;
+  uint32_t tiles_x;       // ceil(cols / 8)
+  uint32_t _pad;
+  uint64_t n_items;       // padded tile items, or offset count
+  const uint32_t* pixel_index;  // offsets mode (NULL = rectangle mode)
+  const double* dx;
+  const double* dy;
+};
+
+struct Outputs {
+  float* xyza;        // 4 floats per sample
+  uint8_t* cls;
+  uint8_t* status;
+  double* xyza64;     // optional
+  uint32_t* steps;    // optional
+  uint8_t* stop;      // optional
+};
+
+}  // namespace grt

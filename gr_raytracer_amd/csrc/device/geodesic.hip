@@ -1,0 +1,1150 @@
+// geodesic.hip — gfx950 kernels for the per-pixel geodesic hot path.
+//
+// One lane traces one camera ray from creation to final colour, entirely in VGPRs:
+//   camera ray (camera.rs:214-254) -> RKF45 attempts (runge_kutta.rs:86-182)
+//   -> for every accepted step: chord window test against every object
+//      (objects.rs:65-120, disc.rs:41-88, sphere.rs:37-128), emitter redshift +
+//      temperature + texture (redshift.rs, temperature.rs, texture.rs), then the
+//      stop test (integrator.rs:203-268)
+//   -> terminal colour + back-to-front blend (scene.rs:153-219).
+// The reference stores the whole trajectory (Vec<Step>, 112 B/step) and runs the
+// window pass afterwards; here the window test is fused into the step loop, which
+// visits exactly the same windows in the same order, so no trajectory ever leaves
+// the register file.
+//
+// The grid is persistent: each wave pulls 64-item chunks of work from one global
+// counter, and whenever lanes finish their ray a wave ballot hands them the next
+// items (lane refill), so long (near-photon-sphere) and short (captured) rays never
+// leave lanes idle until the queue is empty.
+//
+// Floating point follows the reference's evaluation order (Rust, no contraction);
+// the library is compiled with -ffp-contract=off.  Per-frame constants that need
+// libm (sin/cos of the camera position, tan(alpha/2), LUTs) are evaluated on the
+// host, so only per-step transcendentals use the device libm (OCML).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/grt_api.h"
+#include "dev_scene.h"
+#include "kernels.h"
+
+namespace grt {
+
+#define GDEV __device__ __forceinline__
+
+constexpr double PI = 3.14159265358979323846;
+constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
+
+// runge_kutta.rs:16-84
+constexpr double B21 = 2.0 / 9.0;
+constexpr double B31 = 1.0 / 12.0, B32 = 1.0 / 4.0;
+constexpr double B41 = 69.0 / 128.0, B42 = -243.0 / 128.0, B43 = 135.0 / 64.0;
+constexpr double B51 = -17.0 / 12.0, B52 = 27.0 / 4.0, B53 = -27.0 / 5.0, B54 = 16.0 / 15.0;
+constexpr double B61 = 65.0 / 432.0, B62 = -5.0 / 16.0, B63 = 13.0 / 16.0, B64 = 4.0 / 27.0,
+                 B65 = 5.0 / 144.0;
+constexpr double CH1 = 47.0 / 450.0, CH2 = 0.0, CH3 = 12.0 / 25.0, CH4 = 32.0 / 225.0,
+                 CH5 = 1.0 / 30.0, CH6 = 6.0 / 25.0;
+constexpr double CT1 = 1.0 / 150.0, CT2 = 0.0, CT3 = -3.0 / 100.0, CT4 = 16.0 / 75.0,
+                 CT5 = 1.0 / 20.0, CT6 = -6.0 / 25.0;
+constexpr double BETA = 0.9;
+constexpr double INV_ORDER = 1.0 / 5.0;
+constexpr double SMALL_ERR = 1e-5;
+constexpr int MAX_RETRY = 100;
+constexpr double H_MAX = 1.0, H_MIN = 1e-12, H_GROWTH = 4.0;
+
+GDEV double rclamp(double v, double lo, double hi) {  // f64::clamp
+  if (v < lo) v = lo;
+  if (v > hi) v = hi;
+  return v;
+}
+GDEV double rem_euclid(double x, double m) {
+  double r = fmod(x, m);
+  return r < 0.0 ? r + fabs(m) : r;
+}
+GDEV uint32_t sat_u32(double v) {
+  if (!(v > 0.0)) return 0u;
+  if (v >= 4294967296.0) return 0xffffffffu;
+  return (uint32_t)v;
+}
+GDEV uint64_t sat_u64(double v) {
+  if (!(v > 0.0)) return 0ull;
+  if (v >= 18446744073709551616.0) return ~0ull;
+  return (uint64_t)v;
+}
+
+struct XYZA {
+  double x, y, z, a;
+};
+
+// color.rs:49-69  ("other over self")
+GDEV XYZA blend(const XYZA& self, const XYZA& other) {
+  double ab = rclamp(self.a, 0.0, 1.0);
+  double af = rclamp(other.a, 0.0, 1.0);
+  double ao = af + ab * (1.0 - af);
+  if (ao <= 0.0) return XYZA{0.0, 0.0, 0.0, 0.0};
+  XYZA r;
+  r.x = (other.x * af + self.x * ab * (1.0 - af)) / ao;
+  r.y = (other.y * af + self.y * ab * (1.0 - af)) / ao;
+  r.z = (other.z * af + self.z * ab * (1.0 - af)) / ao;
+  r.a = ao;
+  return r;
+}
+
+// Per-ray constants: observer energy (redshift.rs:40-60) and, for KerrBL, the
+// conserved E, L_z, Carter Q (kerr_bl.rs:505-577).
+struct RayConst {
+  double obs;
+  double e, lz, q;
+};
+
+// =========================================================== geometry kernels ======
+// ---- Kerr-Schild helpers (kerr.rs:31-110) ----
+GDEV double ks_r_sqr(double a, double x, double y, double z) {
+  double rho_sqr = x * x + y * y + z * z;
+  return 0.5 * (rho_sqr - a * a + sqrt((rho_sqr - a * a) * (rho_sqr - a * a) + 4.0 * a * a * z * z));
+}
+// metric(): symmetric by construction; returns the 10 distinct entries in g.
+GDEV void ks_metric(double radius, double a, double x, double y, double z, double g[4][4]) {
+  double r_sqr = ks_r_sqr(a, x, y, z);
+  double r = sqrt(r_sqr);
+  double f = (r * r * r * radius) / (r * r * r * r + a * a * z * z);
+  double k_0 = 1.0;
+  double k_x = (r * x + a * y) / (r_sqr + a * a);
+  double k_y = (r * y - a * x) / (r_sqr + a * a);
+  double k_z = z / r;
+  g[0][0] = k_0 * k_0 * f - 1.0;
+  g[0][1] = k_0 * k_x * f;
+  g[0][2] = k_0 * k_y * f;
+  g[0][3] = k_0 * k_z * f;
+  g[1][1] = k_x * k_x * f + 1.0;
+  g[1][2] = k_x * k_y * f;
+  g[1][3] = k_x * k_z * f;
+  g[2][2] = k_y * k_y * f + 1.0;
+  g[2][3] = k_y * k_z * f;
+  g[3][3] = k_z * k_z * f + 1.0;
+  g[1][0] = g[0][1];
+  g[2][0] = g[0][2];
+  g[2][1] = g[1][2];
+  g[3][0] = g[0][3];
+  g[3][1] = g[1][3];
+  g[3][2] = g[2][3];
+}
+GDEV void ks_metric_contra(double radius, double a, double x, double y, double z, double g[4][4]) {
+  double r_sqr = ks_r_sqr(a, x, y, z);
+  double r = sqrt(r_sqr);
+  double f = (r * r * r * radius) / (r * r * r * r + a * a * z * z);
+  double kc[4];
+  kc[0] = -1.0;
+  kc[1] = (r * x + a * y) / (r_sqr + a * a);
+  kc[2] = (r * y - a * x) / (r_sqr + a * a);
+  kc[3] = z / r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double eta = (i == j) ? (i == 0 ? -1.0 : 1.0) : 0.0;
+      g[i][j] = eta - f * kc[i] * kc[j];
+    }
+}
+// nalgebra gemv order: y_i = A_i0 x_0; y_i = A_ik x_k + y_i
+GDEV void mat_vec(const double A[4][4], const double* x, double* y) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double s = A[i][0] * x[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) s = A[i][k] * x[k] + s;
+    y[i] = s;
+  }
+}
+GDEV double quad_form(const double* v, const double M[4][4], const double* w) {
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double r = v[0] * M[0][j];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) r = v[k] * M[k][j] + r;
+    s = (j == 0) ? r * w[0] : r * w[j] + s;
+  }
+  return s;
+}
+
+// kerr.rs:149-186 + :228-235: returns 0.5 * p^T (G dG_i G) p, which equals
+// -0.5 * p^T d_matrix_contravariant(i) p exactly (negation commutes with rounding).
+GDEV double ks_accel(double radius, double a, int index, double x, double y, double z,
+                     const double G[4][4], const double* p) {
+  double c = index == 1 ? x : (index == 2 ? y : z);
+  double h = 1e-10 * fmax(fabs(c), 1.0);
+  double dx = index == 1 ? h : 0.0, dy = index == 2 ? h : 0.0, dz = index == 3 ? h : 0.0;
+  double mp[4][4], mm[4][4];
+  ks_metric(radius, a, x + dx, y + dy, z + dz, mp);
+  ks_metric(radius, a, x - dx, y - dy, z - dz, mm);
+  double two_h = 2.0 * h;
+  double D[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) D[i][j] = (mp[i][j] - mm[i][j]) / two_h;
+  double GD[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double s = G[i][0] * D[0][j];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) s = G[i][k] * D[k][j] + s;
+      GD[i][j] = s;
+    }
+  // stream the columns of (GD)G straight into the quadratic form
+  double q = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double col[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double s = GD[i][0] * G[0][j];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) s = GD[i][k] * G[k][j] + s;
+      col[i] = s;
+    }
+    double r = p[0] * col[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) r = p[k] * col[k] + r;
+    q = (j == 0) ? r * p[0] : r * p[j] + q;
+  }
+  return 0.5 * q;
+}
+
+// ---- KerrBL helpers (kerr_bl.rs:62-118, :253-272) ----
+GDEV double bl_delta(double r, double r_s, double a) { return r * r - r_s * r + a * a; }
+GDEV void metric_bl(double r_s, double a, double r, double sin_t, double cos_t, double g[4][4]) {
+  double sig = r * r + a * a * (cos_t * cos_t);
+  double sin2 = sin_t * sin_t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[i][j] = 0.0;
+  g[0][0] = -(1.0 - r_s * r / sig);
+  g[1][1] = sig / bl_delta(r, r_s, a);
+  g[2][2] = sig;
+  g[3][3] = (r * r + a * a + a * a * r_s * r * sin2 / sig) * sin2;
+  double g_tph = -a * r_s * r * sin2 / sig;
+  g[0][3] = g_tph;
+  g[3][0] = g_tph;
+}
+
+// ---- the ODE right-hand sides ----
+template <int G>
+GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o) {
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {  // schwarzschild.rs:54-80
+    double radius = S.radius;
+    double r = y[1], theta = y[2];
+    double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
+    double st, ct;
+    sincos(theta, &st, &ct);
+    double a = 1.0 - radius / r;
+    double a_prime = radius / (r * r);
+    double aprime_over_a = a_prime / a;
+    double two_over_r = 2.0 / r;
+    o[0] = v_t;
+    o[1] = v_r;
+    o[2] = v_theta;
+    o[3] = v_phi;
+    o[4] = -(aprime_over_a)*v_t * v_r;
+    o[5] = -0.5 * a * a_prime * v_t * v_t + 0.5 * (aprime_over_a)*v_r * v_r +
+           a * r * (v_theta * v_theta + v_phi * v_phi * st * st);
+    o[6] = -(two_over_r)*v_r * v_theta + st * ct * v_phi * v_phi;
+    o[7] = -(two_over_r)*v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
+  } else if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:141-174
+    double radius = S.radius, a = S.a, e = rc.e, l_z = rc.lz, q = rc.q;
+    double r = y[1], theta = y[2];
+    double st, ct;
+    sincos(theta, &st, &ct);
+    double del = bl_delta(r, radius, a);
+    double r2a2 = r * r + a * a;
+    double p_r = r2a2 * e - a * l_z;
+    double sin2 = st * st;
+    o[0] = r2a2 / del * p_r + a * (l_z - a * e * sin2);
+    o[1] = y[4];
+    o[2] = y[5];
+    o[3] = a / del * p_r + l_z / sin2 - a * e;
+    double le = l_z - a * e;
+    double carter = le * le + q;
+    o[4] = (4.0 * r * e * p_r - (2.0 * r - radius) * carter) / 2.0;
+    o[5] = (-2.0 * a * a * e * e * ct * st + 2.0 * l_z * l_z * ct / (st * (st * st))) / 2.0;
+    o[6] = 0.0;
+    o[7] = 0.0;
+  } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:200-241
+    double radius = S.radius, a = S.a;
+    double x = y[1], yy = y[2], z = y[3];
+    double p[4] = {y[4], y[5], y[6], y[7]};
+    double Gc[4][4];
+    ks_metric_contra(radius, a, x, yy, z, Gc);
+    double xdot[4];
+    mat_vec(Gc, p, xdot);
+    o[0] = xdot[0];
+    o[1] = xdot[1];
+    o[2] = xdot[2];
+    o[3] = xdot[3];
+    o[4] = 0.0;
+    o[5] = ks_accel(radius, a, 1, x, yy, z, Gc, p);
+    o[6] = ks_accel(radius, a, 2, x, yy, z, Gc, p);
+    o[7] = ks_accel(radius, a, 3, x, yy, z, Gc, p);
+  } else {  // Euclidean, euclidean.rs:47-53
+    o[0] = y[4];
+    o[1] = y[5];
+    o[2] = y[6];
+    o[3] = y[7];
+    o[4] = 0.0;
+    o[5] = 0.0;
+    o[6] = 0.0;
+    o[7] = 0.0;
+  }
+}
+
+// Number of state components that can be non-zero: KerrBL's y[6], y[7] are
+// identically 0 (its RHS returns literal zeros), so every RKF term on them is an
+// exact +-0 and the norm term a2 + a6 == a2; skipping them is bit-exact.
+template <int G>
+struct Dim {
+  static constexpr int D = (G == GRT_GEOM_KERR_BL) ? 6 : 8;
+};
+
+// One rkf45_step (runge_kutta.rs:86-125).  Returns the truncation error norm.
+template <int G>
+GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
+                        double* yn) {
+  constexpr int D = Dim<G>::D;
+  double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
+  rhs<G>(S, rc, y, o);
+#pragma unroll
+  for (int i = 0; i < D; ++i) k1[i] = h * o[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
+  if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
+  rhs<G>(S, rc, tmp, o);
+#pragma unroll
+  for (int i = 0; i < D; ++i) k2[i] = h * o[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * k1[i] + B32 * k2[i];
+  rhs<G>(S, rc, tmp, o);
+#pragma unroll
+  for (int i = 0; i < D; ++i) k3[i] = h * o[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * k1[i] + B42 * k2[i] + B43 * k3[i];
+  rhs<G>(S, rc, tmp, o);
+#pragma unroll
+  for (int i = 0; i < D; ++i) k4[i] = h * o[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * k1[i] + B52 * k2[i] + B53 * k3[i] + B54 * k4[i];
+  rhs<G>(S, rc, tmp, o);
+#pragma unroll
+  for (int i = 0; i < D; ++i) k5[i] = h * o[i];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    tmp[i] = y[i] + B61 * k1[i] + B62 * k2[i] + B63 * k3[i] + B64 * k4[i] + B65 * k5[i];
+  rhs<G>(S, rc, tmp, o);
+#pragma unroll
+  for (int i = 0; i < D; ++i) k6[i] = h * o[i];
+  double e[8];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    yn[i] = y[i] + CH1 * k1[i] + CH2 * k2[i] + CH3 * k3[i] + CH4 * k4[i] + CH5 * k5[i] + CH6 * k6[i];
+    e[i] = CT1 * k1[i] + CT2 * k2[i] + CT3 * k3[i] + CT4 * k4[i] + CT5 * k5[i] + CT6 * k6[i];
+  }
+  if (D < 8) {
+    yn[6] = 0.0;
+    yn[7] = 0.0;
+  }
+  // nalgebra norm(): 8-accumulator unrolled dot, ((a0+a4) + (a1+a5)) + (a2+a6) + (a3+a7)
+  double res;
+  if constexpr (D == 8) {
+    res = e[0] * e[0] + e[4] * e[4];
+    res += e[1] * e[1] + e[5] * e[5];
+    res += e[2] * e[2] + e[6] * e[6];
+    res += e[3] * e[3] + e[7] * e[7];
+  } else {
+    res = e[0] * e[0] + e[4] * e[4];
+    res += e[1] * e[1] + e[5] * e[5];
+    res += e[2] * e[2];
+    res += e[3] * e[3];
+  }
+  return sqrt(res);
+}
+
+// ---- chart helpers ----
+// Cartesian spatial position of a state (scene.rs:48-69 get_position / point.rs:125-154).
+template <int G>
+GDEV void to_cart(const DevScene& S, const double* y, double* c) {
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
+    double st, ct, sp, cp;
+    sincos(y[2], &st, &ct);
+    sincos(y[3], &sp, &cp);
+    double r = y[1];
+    c[0] = r * st * cp;
+    c[1] = r * st * sp;
+    c[2] = r * ct;
+  } else if constexpr (G == GRT_GEOM_KERR_BL) {
+    double a = S.a, r = y[1];
+    double st, ct, sp, cp;
+    sincos(y[2], &st, &ct);
+    sincos(y[3], &sp, &cp);
+    c[0] = (r * cp - a * sp) * st;
+    c[1] = (r * sp + a * cp) * st;
+    c[2] = r * ct;
+  } else {
+    c[0] = y[1];
+    c[1] = y[2];
+    c[2] = y[3];
+  }
+}
+
+// cartesian_to_spherical (spherical_coordinates_helper.rs:5-26): r, theta, phi
+GDEV void cart_to_sph(double x, double y, double z, double* r_o, double* th_o, double* ph_o) {
+  double r = sqrt(x * x + y * y + z * z);
+  if (r == 0.0) {
+    *r_o = 0.0;
+    *th_o = 0.0;
+    *ph_o = 0.0;
+    return;
+  }
+  *r_o = r;
+  *th_o = acos(z / r);
+  *ph_o = atan2(y, x);
+}
+// cartesian_to_boyer_lindquist (spherical_coordinates_helper.rs:44-61)
+GDEV void cart_to_bl(double a, double x, double y, double z, double* r_o, double* th_o, double* ph_o) {
+  double rho_sqr = x * x + y * y + z * z;
+  double d = rho_sqr - a * a;
+  double r_sqr = 0.5 * (rho_sqr - a * a + sqrt(d * d + 4.0 * a * a * z * z));
+  double r = sqrt(r_sqr);
+  *r_o = r;
+  *th_o = (r == 0.0) ? 0.0 : acos(rclamp(z / r, -1.0, 1.0));
+  *ph_o = atan2(r * y - a * x, r * x + a * y);
+}
+
+// momentum_from_state (geometry.rs:29-31; kerr_bl.rs:225-249; kerr.rs:262-273)
+template <int G>
+GDEV void momentum(const DevScene& S, const RayConst& rc, const double* y, double* p) {
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    double a = S.a, e = rc.e, l_z = rc.lz;
+    double r = y[1], theta = y[2], v_r = y[4], v_theta = y[5];
+    double st, ct;
+    sincos(theta, &st, &ct);
+    double del = bl_delta(r, S.radius, a);
+    double sig = r * r + a * a * (ct * ct);
+    double sin2 = st * st;
+    double p_r_term = (r * r + a * a) * e - a * l_z;
+    double dt = (r * r + a * a) / del * p_r_term + a * (l_z - a * e * sin2);
+    double dphi = a / del * p_r_term + l_z / sin2 - a * e;
+    p[0] = dt / sig;
+    p[1] = v_r / sig;
+    p[2] = v_theta / sig;
+    p[3] = dphi / sig;
+  } else if constexpr (G == GRT_GEOM_KERR) {
+    double Gc[4][4];
+    ks_metric_contra(S.radius, S.a, y[1], y[2], y[3], Gc);
+    mat_vec(Gc, y + 4, p);
+  } else {
+    p[0] = y[4];
+    p[1] = y[5];
+    p[2] = y[6];
+    p[3] = y[7];
+  }
+}
+
+// inner_product at a native-chart point whose polar-angle sin/cos are given.
+template <int G>
+GDEV double inner(const DevScene& S, const double* pos, double st, double ct, const double* v,
+                  const double* w) {
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {  // schwarzschild.rs:90-102
+    double r = pos[1];
+    double a = 1.0 - S.radius / r;
+    return a * v[0] * w[0] - v[1] * w[1] / a - r * r * v[2] * w[2] - r * r * st * st * v[3] * w[3];
+  } else if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:338-359
+    double g[4][4];
+    metric_bl(S.radius, S.a, pos[1], st, ct, g);
+    double result = 0.0;
+#pragma unroll
+    for (int mu = 0; mu < 4; ++mu)
+#pragma unroll
+      for (int nu = 0; nu < 4; ++nu) result += g[mu][nu] * v[mu] * w[nu];
+    return result;
+  } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:283-287
+    double g[4][4];
+    ks_metric(S.radius, S.a, pos[1], pos[2], pos[3], g);
+    return quad_form(v, g, w);
+  } else {  // euclidean.rs:62-67
+    return 1.0 * v[0] * w[0] + -v[1] * w[1] + -v[2] * w[2] + -v[3] * w[3];
+  }
+}
+template <int G>
+GDEV double signature0() {
+  return (G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) ? -1.0 : 1.0;
+}
+
+// get_stationary_velocity_at (schwarzschild.rs:237-240; kerr.rs:449-455; kerr_bl.rs:362-371)
+template <int G>
+GDEV void stationary_velocity(const DevScene& S, const double* pos, double ct, double* u) {
+  u[1] = 0.0;
+  u[2] = 0.0;
+  u[3] = 0.0;
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
+    double a = 1.0 - S.radius / pos[1];
+    u[0] = 1.0 / sqrt(a);
+  } else if constexpr (G == GRT_GEOM_KERR_BL) {
+    double r = pos[1];
+    double sig = r * r + S.a * S.a * (ct * ct);
+    u[0] = 1.0 / sqrt(1.0 - S.radius * r / sig);
+  } else if constexpr (G == GRT_GEOM_KERR) {
+    double a = S.a, z = pos[3];
+    double r_sqr = ks_r_sqr(a, pos[1], pos[2], pos[3]);
+    double r = sqrt(r_sqr);
+    double f = (r * r * r * S.radius) / (r * r * r * r + a * a * z * z);
+    u[0] = 1.0 / sqrt(1.0 - f);
+  } else {
+    u[0] = 1.0;
+  }
+}
+
+// circular_orbit::killing_coefficients (circular_orbit.rs:76-108)
+GDEV bool killing_coefficients(const DevScene& S, double r, double* u_t, double* u_phi) {
+  double r_s = S.radius, a = S.a;
+  double m = 0.5 * r_s;
+  double sqrt_m = sqrt(m);
+  double omega = sqrt_m / (pow(r, 1.5) + a * sqrt_m);
+  double c = S.cos_half_pi, s = S.sin_half_pi;
+  double sig = r * r + a * a * (c * c);
+  double sin2 = s * s;
+  double g_tt = -(1.0 - r_s * r / sig);
+  double g_tphi = -a * r_s * r * sin2 / sig;
+  double g_phiphi = (r * r + a * a + a * a * r_s * r * sin2 / sig) * sin2;
+  double ut_pre = g_tt + 2.0 * omega * g_tphi + omega * omega * g_phiphi;
+  if (ut_pre >= 0.0) return false;
+  double ut = 1.0 / sqrt(-ut_pre);
+  *u_t = ut;
+  *u_phi = omega * ut;
+  return true;
+}
+
+// ============================================================== shading =========
+GDEV XYZA texel(const DevScene& S, const DevTexture& t, uint32_t x, uint32_t y) {
+  uint32_t px = t.rgba[(uint64_t)y * t.width + x];
+  double r = S.srgb_lin[px & 0xffu];
+  double g = S.srgb_lin[(px >> 8) & 0xffu];
+  double b = S.srgb_lin[(px >> 16) & 0xffu];
+  XYZA c;  // srgb_to_xyz (color.rs:310-332), nalgebra gemv order
+  c.x = 0.4124564 * r;
+  c.x = 0.3575761 * g + c.x;
+  c.x = 0.1804375 * b + c.x;
+  c.y = 0.2126729 * r;
+  c.y = 0.7151522 * g + c.y;
+  c.y = 0.0721750 * b + c.y;
+  c.z = 0.0193339 * r;
+  c.z = 0.1191920 * g + c.z;
+  c.z = 0.9503041 * b + c.z;
+  c.a = (double)(px >> 24) / 255.0;
+  return c;
+}
+
+GDEV XYZA sample_blackbody(const DevScene& S, double temperature) {  // texture.rs:149-195
+  uint32_t n = S.bb_n;
+  const double* lt = S.bb_log_t;
+  const double* c = S.bb_xyz;
+  double log_t = log10(fmax(temperature, 10.0));
+  if (!isfinite(log_t) || log_t <= lt[0]) return XYZA{c[0], c[1], c[2], 1.0};
+  if (log_t >= lt[n - 1]) return XYZA{c[3 * (n - 1)], c[3 * (n - 1) + 1], c[3 * (n - 1) + 2], 1.0};
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = lo + (hi - lo) / 2;
+    if (lt[mid] <= log_t) lo = mid + 1; else hi = mid;
+  }
+  uint32_t idx = lo == 0 ? 0 : lo - 1;
+  double lt0 = lt[idx], lt1 = lt[idx + 1];
+  const double* c0 = c + 3 * idx;
+  const double* c1 = c + 3 * (idx + 1);
+  double t = (log_t - lt0) / (lt1 - lt0);
+  return XYZA{c0[0] + t * (c1[0] - c0[0]), c0[1] + t * (c1[1] - c0[1]), c0[2] + t * (c1[2] - c0[2]), 1.0};
+}
+
+// TextureMap::color_at_uv (texture.rs:93-257)
+GDEV XYZA texture_color(const DevScene& S, const DevTexture& t, double u, double v, double redshift,
+                        double temperature) {
+  XYZA c;
+  if (t.kind == GRT_TEX_BITMAP) {
+    uint32_t width = t.width, height = t.height;
+    double p_x = (double)width * u;
+    double p_y = (double)height * v;
+    uint32_t xf = min(sat_u32(floor(p_x)), width - 1);
+    uint32_t yf = min(sat_u32(floor(p_y)), height - 1);
+    uint32_t xc = min(sat_u32(ceil(p_x)), width - 1);
+    uint32_t yc = min(sat_u32(ceil(p_y)), height - 1);
+    XYZA c00 = texel(S, t, xf, yf), c01 = texel(S, t, xf, yc);
+    XYZA c11 = texel(S, t, xc, yc), c10 = texel(S, t, xc, yf);
+    double dx = p_x - (double)xf;
+    double dy = p_y - (double)yf;
+    double w00 = (1.0 - dx) * (1.0 - dy);
+    double w01 = (1.0 - dx) * dy;
+    double w10 = dx * (1.0 - dy);
+    double w11 = dx * dy;
+    c.x = w00 * c00.x + w10 * c10.x + w01 * c01.x + w11 * c11.x;
+    c.y = w00 * c00.y + w10 * c10.y + w01 * c01.y + w11 * c11.y;
+    c.z = w00 * c00.z + w10 * c10.z + w01 * c01.z + w11 * c11.z;
+    c.a = w00 * c00.a + w10 * c10.a + w01 * c01.a + w11 * c11.a;
+  } else if (t.kind == GRT_TEX_CHECKER) {
+    uint64_t ut = sat_u64(floor(u * t.cw));
+    uint64_t vt = sat_u64(floor(v * t.ch));
+    const double* cc = ((ut + vt) % 2 == 0) ? t.c1 : t.c2;
+    c = XYZA{cc[0], cc[1], cc[2], cc[3]};
+  } else {
+    c = sample_blackbody(S, temperature * redshift);
+  }
+  double f = pow(redshift, t.beaming);  // apply_beaming (color.rs:72-80)
+  return XYZA{c.x * f, c.y * f, c.z * f, c.a};
+}
+
+// KerrTemperatureComputer::compute_temperature (temperature.rs:198-253)
+GDEV int compute_temperature(const DevObject& o, double radius, double* out) {
+  if (o.temp_kind == GRT_TEMP_CONSTANT) {
+    *out = o.temp_constant;
+    return GRT_OK;
+  }
+  if (!isfinite(radius)) return GRT_ERR_NON_FINITE_RADIUS;
+  if (radius < o.r_isco) return GRT_ERR_BELOW_RISCO;
+  uint32_t n = o.lut_n;
+  if (radius <= o.lut_r[0]) { *out = o.lut_t[0]; return GRT_OK; }
+  if (radius >= o.lut_r[n - 1]) { *out = o.lut_t[n - 1]; return GRT_OK; }
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = lo + (hi - lo) / 2;
+    if (o.lut_r[mid] <= radius) lo = mid + 1; else hi = mid;
+  }
+  uint32_t idx = lo == 0 ? 0 : lo - 1;
+  double r0 = o.lut_r[idx], t0 = o.lut_t[idx], r1 = o.lut_r[idx + 1], t1 = o.lut_t[idx + 1];
+  double t = (radius - r0) / (r1 - r0);
+  *out = t0 + t * (t1 - t0);
+  return GRT_OK;
+}
+
+// ====================================================== window (chord) tests ======
+struct Hit {
+  double u, v, t;
+  double px, py, pz;  // Cartesian (world) intersection point
+};
+
+// disc.rs:41-88.  The sign / magnitude pre-filter only skips divisions whose quotient
+// is provably outside [0, 1]; every accepted t is the same correctly-rounded p1/p2.
+GDEV bool disc_hit(const DevObject& o, const double* s, const double* e, Hit* h) {
+  double d0 = e[0] - s[0], d1 = e[1] - s[1], d2 = e[2] - s[2];
+  double p1 = (0.0 - s[0]) * 0.0 + (0.0 - s[1]) * 0.0 + (0.0 - s[2]) * 1.0;
+  double p2 = d0 * 0.0 + d1 * 0.0 + d2 * 1.0;
+  if ((p1 > 0.0 && p2 < 0.0) || (p1 < 0.0 && p2 > 0.0)) return false;  // t < 0
+  if (fabs(p1) > 2.0 * fabs(p2)) return false;                         // t > 2
+  double t = p1 / p2;
+  if (!(0.0 <= t && t <= 1.0)) return false;
+  double ix = s[0] + t * d0, iy = s[1] + t * d1, iz = s[2] + t * d2;
+  double rr = ix * ix + iy * iy + iz * iz;
+  if (!(rr >= o.rin2 && rr <= o.rout2)) return false;
+  double phi = atan2(iy - 0.0, ix - 0.0);
+  double r = (sqrt(rr) - o.rin) / (o.rout - o.rin);
+  double sp, cp;
+  sincos(phi, &sp, &cp);
+  h->u = 0.5 + 0.5 * r * cp;
+  h->v = 0.5 + 0.5 * r * sp;
+  h->t = t;
+  h->px = ix;
+  h->py = iy;
+  h->pz = iz;
+  return true;
+}
+
+// sphere.rs:37-128
+GDEV bool sphere_hit(const DevObject& o, const double* s_w, const double* e_w, Hit* h) {
+  double s0 = s_w[0] + -o.cx, s1 = s_w[1] + -o.cy, s2 = s_w[2] + -o.cz;
+  double e0 = e_w[0] + -o.cx, e1 = e_w[1] + -o.cy, e2 = e_w[2] + -o.cz;
+  double r_start = s0 * s0 + s1 * s1 + s2 * s2;
+  double r_end = e0 * e0 + e1 * e1 + e2 * e2;
+  double R2 = o.R2;
+  if (!((r_start >= R2 && r_end <= R2) || (r_start <= R2 && r_end >= R2))) return false;
+  double d0 = e0 - s0, d1 = e1 - s1, d2 = e2 - s2;
+  double a = d0 * d0 + d1 * d1 + d2 * d2;
+  double b = 2.0 * (s0 * d0 + s1 * d1 + s2 * d2);
+  double c = (s0 * s0 + s1 * s1 + s2 * s2) - o.radius * o.radius;
+  double disc = b * b - 4.0 * a * c;
+  if (disc < 0.0) return false;
+  double sq = sqrt(disc);
+  double t1 = (-b + sq) / (2.0 * a);
+  double t2 = (-b - sq) / (2.0 * a);
+  double t;
+  if (0.0 <= t1 && t1 <= 1.0) t = t1;
+  else if (0.0 <= t2 && t2 <= 1.0) t = t2;
+  else return false;
+  double px = s0 + t * d0, py = s1 + t * d1, pz = s2 + t * d2;
+  double rr, theta, phi;
+  cart_to_sph(px, py, pz, &rr, &theta, &phi);
+  double u = (PI + phi) / TWO_PI;
+  h->u = 1.0 - u;
+  h->v = theta / PI;
+  h->t = t;
+  h->px = px + o.cx;
+  h->py = py + o.cy;
+  h->pz = pz + o.cz;
+  return true;
+}
+
+// Emitter step at the intersection (objects.rs:27-44 + :95-115) and its colour.
+// Returns a grt_status; on success *col holds the hit colour.
+template <int G>
+GDEV int shade_hit(const DevScene& S, const RayConst& rc, const DevObject& o, const Hit& h,
+                   const double* ys, const double* ye, XYZA* col) {
+  // step.x = intersection point converted to the native chart
+  double x[4];
+  double st, ct;
+  x[0] = 0.0;
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
+    cart_to_sph(h.px, h.py, h.pz, &x[1], &x[2], &x[3]);
+    sincos(x[2], &st, &ct);
+  } else if constexpr (G == GRT_GEOM_KERR_BL) {
+    cart_to_bl(S.a, h.px, h.py, h.pz, &x[1], &x[2], &x[3]);
+    sincos(x[2], &st, &ct);
+  } else {
+    x[1] = h.px;
+    x[2] = h.py;
+    x[3] = h.pz;
+    st = 0.0;
+    ct = 0.0;
+  }
+  // step.p = lerp of the window's endpoint momenta
+  double pa[4], pb[4], p[4];
+  momentum<G>(S, rc, ys, pa);
+  momentum<G>(S, rc, ye, pb);
+  double sw = 1.0 - h.t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) p[i] = sw * pa[i] + h.t * pb[i];
+  double u[4];
+  if (o.kind == GRT_OBJ_DISC) {  // disc.rs:101-110: circular-orbit emitter
+    if constexpr (G == GRT_GEOM_EUCLIDEAN) {
+      u[0] = 1.0; u[1] = 0.0; u[2] = 0.0; u[3] = 0.0;
+    } else {
+      double r;
+      if constexpr (G == GRT_GEOM_KERR) r = sqrt(ks_r_sqr(S.a, x[1], x[2], x[3]));
+      else r = x[1];
+      double ut, uphi;
+      if (!killing_coefficients(S, r, &ut, &uphi)) return GRT_ERR_NO_CIRCULAR_ORBIT;
+      if constexpr (G == GRT_GEOM_KERR) {
+        double ax[4] = {0.0, -x[2], x[1], 0.0};
+        double et[4] = {1.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[i] = ut * et[i] + uphi * ax[i];
+      } else {
+        u[0] = ut; u[1] = 0.0; u[2] = 0.0; u[3] = uphi;
+      }
+    }
+  } else {  // sphere.rs:141-150: static emitter
+    stationary_velocity<G>(S, x, ct, u);
+  }
+  double em = inner<G>(S, x, st, ct, u, p);
+  double sig0 = signature0<G>();
+  double redshift = (sig0 * rc.obs) / (sig0 * em);
+  double temperature;
+  if (o.kind == GRT_OBJ_DISC) {
+    double rad;  // get_radial_coordinate of the Cartesian intersection point
+    if constexpr (G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) {
+      rad = sqrt(ks_r_sqr(S.a, h.px, h.py, h.pz));
+    } else {
+      rad = sqrt(h.px * h.px + h.py * h.py + h.pz * h.pz);
+    }
+    int e = compute_temperature(o, rad, &temperature);
+    if (e != GRT_OK) return e;
+  } else {
+    temperature = o.temperature;
+  }
+  *col = texture_color(S, o.tex, h.u, h.v, redshift, temperature);
+  return GRT_OK;
+}
+
+// ============================================================== kernel ==========
+template <int G>
+struct Lane {
+  double y[8], yp[8];
+  double c[3], cp[3];
+  double t, h, h_cur;
+  uint64_t i;
+  int retries;
+  RayConst rc;
+  double opacity;
+  int nhits;
+  int status;
+  uint32_t steps;
+};
+
+// camera.rs:214-232 get_direction_for, then momentum = direction - e_t (:243, :252)
+GDEV void camera_momentum(const DevCamera& c, double row, double column, double* p) {
+  double shifted_column = column + 1.0;
+  double shifted_row = row + 1.0;
+  double tha = c.tan_half_alpha;
+  double i_prime = c.hand * (2.0 * tha / c.rows) * (shifted_column - (c.cols + 1.0) / 2.0);
+  double j_prime = (2.0 * tha / c.rows) * (shifted_row - (c.rows + 1.0) / 2.0);
+  double w_squared = c.sig_s * (1.0 + i_prime * i_prime + j_prime * j_prime);
+  double denom = c.sig_s * w_squared;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double w = c.tet[3][k] + i_prime * c.tet[1][k] + j_prime * c.tet[2][k];
+    double dir = -c.tet[3][k] + 2.0 * w / denom;
+    p[k] = dir + (-c.tet[0][k]);
+  }
+}
+
+// Create the ray state (integrator.rs:82-99 + geometry-specific create_initial_state).
+template <int G>
+GDEV void init_ray(const DevScene& S, Lane<G>& L, double row, double col) {
+  const DevCamera& cam = S.cam;
+  double p[4];
+  camera_momentum(cam, row, col, p);
+  // observer energy at the camera (redshift.rs:40-43), camera sin/cos from the host
+  L.rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
+  L.rc.e = 0.0;
+  L.rc.lz = 0.0;
+  L.rc.q = 0.0;
+  if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:505-577, :176-223 (BL ray)
+    double a = S.a, radius = S.radius;
+    double r = cam.pos[1];
+    double st = cam.sin_theta, ct = cam.cos_theta;
+    double g[4][4];
+    metric_bl(radius, a, r, st, ct, g);
+    double pc[4];
+    mat_vec(g, p, pc);
+    double e = -pc[0], l_z = pc[3], p_theta = pc[2];
+    double sin2 = st * st;
+    double q = p_theta * p_theta + ct * ct * (l_z * l_z / fmax(sin2, 1e-28) - a * a * e * e);
+    L.rc.e = e;
+    L.rc.lz = l_z;
+    L.rc.q = q;
+    double sign_r = p[1] >= 0.0 ? 1.0 : -1.0;
+    double sign_theta = p[2] >= 0.0 ? 1.0 : -1.0;
+    double del = bl_delta(r, radius, a);
+    double p_r = (r * r + a * a) * e - a * l_z;
+    double le = l_z - a * e;
+    double r_pot = p_r * p_r - del * (le * le + q);
+    double th_pot = q + a * a * e * e * ct * ct - l_z * l_z * ct * ct / (st * st);
+    L.y[0] = cam.pos[0];
+    L.y[1] = r;
+    L.y[2] = cam.pos[2];
+    L.y[3] = cam.pos[3];
+    L.y[4] = sign_r * sqrt(fmax(r_pot, 0.0));
+    L.y[5] = sign_theta * sqrt(fmax(th_pot, 0.0));
+    L.y[6] = 0.0;
+    L.y[7] = 0.0;
+  } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:243-260
+    double g[4][4];
+    ks_metric(S.radius, S.a, cam.pos[1], cam.pos[2], cam.pos[3], g);
+    double pc[4];
+    mat_vec(g, p, pc);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      L.y[k] = cam.pos[k];
+      L.y[4 + k] = pc[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      L.y[k] = cam.pos[k];
+      L.y[4 + k] = p[k];
+    }
+  }
+  L.t = 0.0;
+  L.h = S.step_size;
+  L.h_cur = rclamp(L.h, H_MIN, H_MAX);
+  L.i = 0;
+  L.retries = 0;
+  L.opacity = 0.0;
+  L.nhits = 0;
+  L.status = GRT_OK;
+  L.steps = 0;
+  to_cart<G>(S, L.y, L.c);
+}
+
+// integrator.rs:203-268
+template <int G>
+GDEV int should_stop(const DevScene& S, const double* y, const double* c, uint64_t i) {
+  if (!(isfinite(y[0]) && isfinite(y[1]) && isfinite(y[2]) && isfinite(y[3]))) return GRT_STOP_NAN;
+  bool last = (i == S.max_steps - 1);
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
+    if (G == GRT_GEOM_SCHWARZSCHILD || S.has_horizon) {
+      if (y[1] <= S.horizon_r) return GRT_STOP_HORIZON;
+    }
+    if (last && y[1] < S.trapped_radius) return GRT_STOP_CLOSED_ORBIT;
+  } else if constexpr (G == GRT_GEOM_KERR) {
+    double r = sqrt(ks_r_sqr(S.a, y[1], y[2], y[3]));
+    if (S.has_horizon && r <= S.horizon_r) return GRT_STOP_HORIZON;
+    if (last && r < S.trapped_radius) return GRT_STOP_CLOSED_ORBIT;
+  }
+  if (c[0] * c[0] + c[1] * c[1] + c[2] * c[2] > S.max_radius_sq) return GRT_STOP_CELESTIAL;
+  if (!(isfinite(y[4]) && isfinite(y[5]) && isfinite(y[6]) && isfinite(y[7]))) return GRT_STOP_NAN;
+  return GRT_STOP_NONE;
+}
+
+// Terminal colour + back-to-front blend (scene.rs:153-219).
+template <int G>
+GDEV XYZA finalize_color(const DevScene& S, const Lane<G>& L, int stop, const XYZA* hits, int* cls) {
+  XYZA result{0.0, 0.0, 0.0, 1.0};
+  *cls = GRT_CLASS_CAPTURED;
+  if (stop == GRT_STOP_HORIZON || stop == GRT_STOP_CLOSED_ORBIT) {
+    result = blend(result, XYZA{0.0, 0.0, 0.0, 1.0});
+  } else if (stop == GRT_STOP_CELESTIAL) {
+    const double* y = L.y;
+    double th, ph;  // get_as_spherical (point.rs:172-188)
+    double st, ct;
+    if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
+      th = rem_euclid(y[2], PI);
+      ph = rem_euclid(y[3] + PI, TWO_PI) - PI;
+      sincos(y[2], &st, &ct);
+    } else {
+      double rr;
+      cart_to_sph(y[1], y[2], y[3], &rr, &th, &ph);
+      st = 0.0;
+      ct = 0.0;
+    }
+    double u = (PI + ph) / TWO_PI;
+    double v = th / PI;
+    double vel[4], p[4];
+    stationary_velocity<G>(S, y, ct, vel);
+    momentum<G>(S, L.rc, y, p);
+    double em = inner<G>(S, y, st, ct, vel, p);
+    double sig0 = signature0<G>();
+    double redshift = (sig0 * L.rc.obs) / (sig0 * em);
+    result = blend(result, texture_color(S, S.celestial, 1.0 - u, v, redshift, S.celestial_temperature));
+    *cls = GRT_CLASS_ESCAPED;
+  }
+  int n = L.nhits < GRT_MAX_HITS ? L.nhits : GRT_MAX_HITS;
+  for (int k = n - 1; k >= 0; --k) result = blend(result, hits[k]);
+  if (L.opacity >= S.hit_threshold) *cls = GRT_CLASS_HIT;
+  return result;
+}
+
+GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, int status, int stop,
+                    uint32_t steps) {
+  reinterpret_cast<float4*>(out.xyza)[idx] = make_float4((float)c.x, (float)c.y, (float)c.z, (float)c.a);
+  out.cls[idx] = (uint8_t)cls;
+  out.status[idx] = (uint8_t)status;
+  if (out.xyza64) {
+    double* d = out.xyza64 + 4 * idx;
+    d[0] = c.x;
+    d[1] = c.y;
+    d[2] = c.z;
+    d[3] = c.a;
+  }
+  if (out.steps) out.steps[idx] = steps;
+  if (out.stop) out.stop[idx] = (uint8_t)stop;
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) trace_kernel(const DevScene* __restrict__ Sp, WorkList wl,
+                                                    Outputs out,
+                                                    unsigned long long* __restrict__ counter,
+                                                    unsigned long long* __restrict__ stats) {
+  const DevScene& S = *Sp;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  constexpr uint64_t CHUNK = 64;
+
+  uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
+  bool active = false, done = false;
+  uint64_t out_idx = 0;
+  Lane<G> L;
+  XYZA hits[GRT_MAX_HITS];
+  uint64_t n_acc = 0, n_att = 0, n_rays = 0, n_over = 0;
+
+  while (true) {
+    // ---------------- lane refill: ballot, one atomic per 64 items --------------
+    bool need = !active && !done;
+    uint64_t need_mask = __ballot(need);
+    if (need_mask) {
+      uint64_t cnt = __popcll(need_mask);
+      uint64_t remaining = chunk_end - chunk_next;
+      uint64_t new_base = 0;
+      if (cnt > remaining) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(counter, (unsigned long long)CHUNK);
+        new_base = __shfl(b, 0);
+      }
+      if (need) {
+        uint64_t rank = __popcll(need_mask & lanemask_lt);
+        uint64_t item = rank < remaining ? chunk_next + rank : new_base + (rank - remaining);
+        if (item >= wl.n_items) {
+          done = true;
+        } else {
+          double row, col;
+          bool valid = true;
+          if (wl.pixel_index) {  // offset list (get_ray_for_offset, camera.rs:247-254)
+            uint32_t pix = wl.pixel_index[item];
+            double r = (double)(wl.row0 + pix / wl.cols), cc = (double)(wl.col0 + pix % wl.cols);
+            row = r + (wl.dy[item] - 0.5);
+            col = cc + (wl.dx[item] - 0.5);
+            out_idx = item;
+          } else {  // 8x8 pixel tiles, row-major tiles
+            uint64_t tile = item >> 6;
+            uint32_t w = (uint32_t)(item & 63);
+            uint32_t tr = (uint32_t)(tile / wl.tiles_x), tc = (uint32_t)(tile % wl.tiles_x);
+            uint32_t r = tr * 8 + (w >> 3), cc = tc * 8 + (w & 7);
+            valid = (r < wl.rows) && (cc < wl.cols);
+            row = (double)(wl.row0 + r);
+            col = (double)(wl.col0 + cc);
+            out_idx = (uint64_t)r * wl.cols + cc;
+          }
+          if (valid) {
+            init_ray<G>(S, L, row, col);
+            active = true;
+            n_rays++;
+            if (S.max_steps <= 1) {  // `for i in 1..max_steps` never runs
+              int cls;
+              XYZA col_ = finalize_color<G>(S, L, GRT_STOP_NONE, hits, &cls);
+              write_out(out, out_idx, col_, cls, GRT_OK, GRT_STOP_NONE, 0);
+              active = false;
+            }
+          }
+        }
+      }
+      if (cnt > remaining) {
+        chunk_next = new_base + (cnt - remaining);
+        chunk_end = new_base + CHUNK;
+      } else {
+        chunk_next += cnt;
+      }
+    }
+    if (__ballot(!done) == 0) break;
+    if (!active) continue;
+
+    // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
+    double yn[8];
+    double err = rkf_attempt<G>(S, L.rc, L.y, L.h_cur, yn);
+    n_att++;
+    double h_prop = err > 0.0 ? BETA * L.h_cur * pow(S.epsilon / err, INV_ORDER) : L.h_cur * H_GROWTH;
+    h_prop = rclamp(fmin(h_prop, L.h_cur * H_GROWTH), H_MIN, H_MAX);
+    bool accept;
+    double h_next = 0.0;
+    if (err > S.epsilon) {
+      if (L.h_cur <= H_MIN) {
+        accept = true;
+        h_next = L.h_cur;
+      } else {
+        accept = false;
+        L.h_cur = rclamp(h_prop / 2.0, H_MIN, H_MAX);
+        if (++L.retries >= MAX_RETRY) {  // Err(MaxStepsReached)
+          write_out(out, out_idx, XYZA{0.0, 0.0, 0.0, 1.0}, GRT_CLASS_ESCAPED, GRT_ERR_MAX_STEPS_REACHED,
+                    GRT_STOP_NONE, L.steps);
+          active = false;
+          continue;
+        }
+      }
+    } else {
+      accept = true;
+      h_next = (err / S.epsilon < SMALL_ERR) ? rclamp(L.h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
+    }
+    if (!accept) continue;
+
+    // ---------------- accepted step i (integrator.rs:100-162) --------------------
+    L.t += L.h_cur;
+    L.h = h_next;
+    L.i++;
+    L.steps++;
+    n_acc++;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      L.yp[k] = L.y[k];
+      L.y[k] = yn[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) L.cp[k] = L.c[k];
+    to_cart<G>(S, L.y, L.c);
+
+    // window (yp -> y) against every object, nearest hit wins (objects.rs:65-120)
+    int werr = GRT_OK;
+    bool has = false;
+    XYZA wcol;
+    double shortest = 1.7976931348623157e308;
+    for (uint32_t k = 0; k < S.n_objects; ++k) {
+      const DevObject& o = S.obj[k];
+      Hit hh;
+      bool hit = (o.kind == GRT_OBJ_DISC) ? disc_hit(o, L.cp, L.c, &hh) : sphere_hit(o, L.cp, L.c, &hh);
+      if (!hit) continue;
+      double dx = hh.px - L.cp[0], dy = hh.py - L.cp[1], dz = hh.pz - L.cp[2];
+      double distance = sqrt(dx * dx + dy * dy + dz * dz);
+      if (distance < shortest) {
+        shortest = distance;
+        XYZA cc;
+        int e = shade_hit<G>(S, L.rc, o, hh, L.yp, L.y, &cc);
+        if (e != GRT_OK) {
+          werr = e;
+          break;
+        }
+        wcol = cc;
+        has = true;
+      }
+    }
+    if (werr != GRT_OK) {  // any window error aborts the pixel (scene.rs:146)
+      write_out(out, out_idx, XYZA{0.0, 0.0, 0.0, 1.0}, GRT_CLASS_ESCAPED, werr, GRT_STOP_NONE, L.steps);
+      active = false;
+      continue;
+    }
+    if (has) {
+      if (L.nhits < GRT_MAX_HITS) hits[L.nhits] = wcol;
+      else L.status |= GRT_FLAG_HIT_OVERFLOW;
+      L.nhits++;
+      double alpha = rclamp(wcol.a, 0.0, 1.0);
+      L.opacity = alpha + L.opacity * (1.0 - alpha);
+    }
+
+    int stop = should_stop<G>(S, L.y, L.c, L.i);
+    if (stop != GRT_STOP_NONE || L.i == S.max_steps - 1) {
+      int cls;
+      XYZA col_ = finalize_color<G>(S, L, stop, hits, &cls);
+      if (L.status & GRT_FLAG_HIT_OVERFLOW) n_over++;
+      write_out(out, out_idx, col_, cls, L.status, stop, L.steps);
+      active = false;
+      continue;
+    }
+    L.retries = 0;
+    L.h_cur = rclamp(L.h, H_MIN, H_MAX);
+  }
+
+  // per-wave reduction of the counters, one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    n_acc += __shfl_down(n_acc, off);
+    n_att += __shfl_down(n_att, off);
+    n_rays += __shfl_down(n_rays, off);
+    n_over += __shfl_down(n_over, off);
+  }
+  if (lane == 0) {
+    atomicAdd(stats + 0, (unsigned long long)n_acc);
+    atomicAdd(stats + 1, (unsigned long long)n_att);
+    atomicAdd(stats + 2, (unsigned long long)n_rays);
+    atomicAdd(stats + 3, (unsigned long long)n_over);
+  }
+}
+
+// ------------------------------------------------------------------ launch -------
+hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Outputs& out,
+                        unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
+                        int threads, hipStream_t stream) {
+  dim3 grid(blocks), block(threads);
+  switch (geometry) {
+    case GRT_GEOM_EUCLIDEAN:
+      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_EUCLIDEAN>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
+      break;
+    case GRT_GEOM_SCHWARZSCHILD:
+      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_SCHWARZSCHILD>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
+      break;
+    case GRT_GEOM_KERR:
+      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_KERR>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
+      break;
+    case GRT_GEOM_KERR_BL:
+      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_KERR_BL>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace grt

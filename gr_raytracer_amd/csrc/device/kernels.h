@@ -1,0 +1,32 @@
+// kernels.h — launch entry points of the gfx950 kernels (geodesic.hip, adaptive.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev_scene.h"
+
+namespace grt {
+
+hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Outputs& out,
+                        unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
+                        int threads, hipStream_t stream);
+
+// Adaptive supersampling helpers (raytracer.rs:91-159, :320-458).
+struct AdaptiveParams {
+  uint32_t w, h;  // section size
+  int32_t exclude_background_contrast;
+  int32_t _pad;
+  double min_lum;
+  double luminance_contrast_threshold;
+  double opacity_contrast_threshold;
+};
+hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const AdaptiveParams& p,
+                         uint8_t* d_flags, hipStream_t stream);
+hipError_t launch_make_offsets(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, uint32_t row0,
+                               uint32_t col0, uint32_t w, uint32_t* d_pix, double* d_dx, double* d_dy,
+                               hipStream_t stream);
+hipError_t launch_average(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, const double* d_samples,
+                          const uint8_t* d_status, double* d_out, hipStream_t stream);
+hipError_t launch_paint(const uint32_t* d_sel, uint64_t n_sel, const double* mask, double* d_out,
+                        hipStream_t stream);
+
+}  // namespace grt

@@ -1,0 +1,54 @@
+// host_internal.h — internal declarations shared by the host-side C++ files.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../../include/grt_api.h"
+
+namespace grt_host {
+
+void set_error(const std::string& msg);
+double rclamp_pub(double v, double lo, double hi);
+int camera_build(int geometry, double radius, double a, const double position[4], const double velocity[4],
+                 double alpha, int64_t rows, int64_t cols, double phi, double theta, double psi,
+                 grt_camera_desc* out);
+bool future_directed(int geometry, double radius, double a, const double position[4], const double v[4]);
+double inner(int geometry, double radius, double a, const double position[4], const double v[4], const double w[4]);
+double signature0(int geometry);
+double r_isco(double r_s, double a);
+int kerr_temperature_lut(double temperature, double outer_radius, double a, double radius, uint32_t n,
+                         double* lut_r, double* lut_t, double* r_isco_out);
+void blackbody_xyz(double temperature, double redshift, double out[3]);
+int blackbody_lut(uint32_t n, double* log_t, double* xyz);
+double inv_compand_srgb(double u);
+void srgb_to_xyza(uint8_t r8, uint8_t g8, uint8_t b8, uint8_t a8, double out[4]);
+int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_t* rgb);
+int stationary(int geometry, double radius, double a, const double position[4], double out[4]);
+int zamo(int geometry, double radius, double a, const double position[4], double out[4]);
+
+// ---- minimal TOML (the subset the reference's scene files use) ----
+struct TomlValue;
+using TomlTable = std::map<std::string, std::shared_ptr<TomlValue>>;
+struct TomlValue {
+  enum Kind { Float, Int, Bool, String, Array, Table, TableArray } kind = Table;
+  double f = 0.0;
+  int64_t i = 0;
+  bool b = false;
+  std::string s;
+  std::vector<std::shared_ptr<TomlValue>> arr;
+  TomlTable table;
+  double number() const { return kind == Int ? (double)i : f; }
+};
+bool toml_parse(const std::string& text, TomlTable& root, std::string& err);
+
+// ---- PNG (8-bit, non-interlaced) ----
+bool png_decode_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& w, uint32_t& h,
+                     std::string& err);
+bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err);
+bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint32_t h, std::string& err);
+
+}  // namespace grt_host

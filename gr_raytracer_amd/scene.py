@@ -1,0 +1,382 @@
+"""Host-side mirror of the reference's scene/render surface, over the C ABI.
+
+Names follow mdreem/gr_raytracer:
+  * GlobalOpts                 src/cli/cli.rs:5-47
+  * load_scene                 main.rs:74-116 + cli/<geometry>.rs + cli/shared.rs:131-321
+  * Scene.render_section       Raytracer::render_section_to_cie_buffer (raytracer.rs:177-318)
+  * Scene.render_pixels        render_section_to_cie_buffer_raw (raytracer.rs:195-244)
+  * Scene.color_of_ray         Scene::color_of_ray (scene.rs:114-220) for one camera pixel
+  * SceneBuilder               scene.rs::test_scene::create_scene_with_camera (scene.rs:250-369)
+Every call runs the HIP kernels in libgrt.so; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+# ------------------------------------------------------------------ options -------
+@dataclass
+class GlobalOpts:
+    """clap GlobalOpts (cli.rs:5-47) with the reference defaults."""
+    width: int = 500
+    height: int = 500
+    step_size: float = 0.01
+    max_steps: int = 20000
+    max_radius: float = 15000.0
+    epsilon: float = 0.00001
+    camera_position: Sequence[float] = (18.0, 0.0, 0.8)
+    phi: float = 0.0
+    theta: float = 0.0
+    psi: float = 0.0
+    tone_mapping: str = "reinhard"
+    show_sampling_mask: bool = False
+    sampling_mask_color: Sequence[int] = (255, 0, 255)
+
+    def to_c(self) -> L.GlobalOpts:
+        o = L.GlobalOpts()
+        L.lib().grt_default_global_opts(C.byref(o))
+        o.width, o.height = int(self.width), int(self.height)
+        o.step_size, o.max_steps, o.max_radius = float(self.step_size), int(self.max_steps), float(self.max_radius)
+        o.epsilon = float(self.epsilon)
+        for k in range(3):
+            o.camera_position[k] = float(self.camera_position[k])
+            o.sampling_mask_color[k] = int(self.sampling_mask_color[k])
+        o.phi, o.theta, o.psi = float(self.phi), float(self.theta), float(self.psi)
+        o.tone_mapping = {"reinhard": 0, "global-linear": 1}[self.tone_mapping]
+        o.show_sampling_mask = int(bool(self.show_sampling_mask))
+        return o
+
+
+def default_adaptive() -> L.AdaptiveConfig:
+    c = L.AdaptiveConfig()
+    L.lib().grt_default_adaptive_config(C.byref(c))
+    return c
+
+
+def device_count() -> int:
+    return int(L.lib().grt_device_count())
+
+
+# ------------------------------------------------------------------ scenes --------
+class HostScene:
+    """A TOML scene built on the host (textures decoded, camera tetrad, LUTs)."""
+
+    def __init__(self, config_file: str, opts: GlobalOpts, resource_root: Optional[str] = None):
+        self._h = C.c_void_p()
+        rr = None if resource_root is None else str(resource_root).encode()
+        L.check(L.lib().grt_host_scene_load(str(config_file).encode(), rr, C.byref(opts.to_c()), C.byref(self._h)),
+                f"load_scene({config_file})")
+        self.opts = opts
+
+    @property
+    def desc(self) -> L.SceneDesc:
+        return L.lib().grt_host_scene_desc(self._h).contents
+
+    def desc_ptr(self):
+        return L.lib().grt_host_scene_desc(self._h)
+
+    @property
+    def adaptive(self) -> L.AdaptiveConfig:
+        c = L.AdaptiveConfig()
+        L.lib().grt_host_scene_adaptive(self._h, C.byref(c))
+        return c
+
+    def close(self) -> None:
+        if self._h:
+            L.lib().grt_host_scene_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_scene(config_file: str, opts: Optional[GlobalOpts] = None, resource_root: Optional[str] = None) -> "Scene":
+    """Parse a scene TOML + options and upload it (main.rs:74-116, cli/shared.rs:131-321)."""
+    hs = HostScene(config_file, opts or GlobalOpts(), resource_root)
+    return Scene(hs.desc_ptr(), keepalive=hs, adaptive=hs.adaptive)
+
+
+@dataclass
+class RenderResult:
+    xyza: np.ndarray                 # float32 (n, 4)
+    ray_class: np.ndarray            # uint8 (n,)
+    status: np.ndarray               # uint8 (n,)
+    xyza64: Optional[np.ndarray] = None
+    steps: Optional[np.ndarray] = None
+    stop_reason: Optional[np.ndarray] = None
+    stats: dict = field(default_factory=dict)
+
+
+def _stats_dict(st: L.Stats) -> dict:
+    return {"accepted_steps": int(st.accepted_steps), "attempts": int(st.attempts), "rays": int(st.rays),
+            "hit_overflows": int(st.hit_overflows), "kernel_ms": float(st.kernel_ms)}
+
+
+class Scene:
+    """Device-resident scene (grt_scene); one device copy per GPU, created lazily."""
+
+    def __init__(self, desc_ptr, keepalive=None, adaptive: Optional[L.AdaptiveConfig] = None):
+        self._s = C.c_void_p()
+        L.check(L.lib().grt_scene_create(desc_ptr, C.byref(self._s)), "grt_scene_create")
+        self._keep = keepalive
+        self.desc = desc_ptr.contents
+        self.adaptive = adaptive if adaptive is not None else default_adaptive()
+
+    @property
+    def rows(self) -> int:
+        return int(self.desc.camera.rows)
+
+    @property
+    def cols(self) -> int:
+        return int(self.desc.camera.cols)
+
+    def close(self) -> None:
+        if self._s:
+            L.lib().grt_scene_destroy(self._s)
+            self._s = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render_pixels(self, row0: int = 0, col0: int = 0, rows: Optional[int] = None, cols: Optional[int] = None,
+                      device: int = 0, offsets=None, aux: bool = True) -> RenderResult:
+        """1-spp trace of a rectangle, or of an offset list (pixel_index, dx, dy)."""
+        rows = self.rows - row0 if rows is None else rows
+        cols = self.cols - col0 if cols is None else cols
+        off = None
+        keep = []
+        if offsets is not None:
+            pix, dx, dy = (np.ascontiguousarray(offsets[0], np.uint32), np.ascontiguousarray(offsets[1], np.float64),
+                           np.ascontiguousarray(offsets[2], np.float64))
+            keep += [pix, dx, dy]
+            off = L.Offsets(len(pix), L.ptr(pix, C.c_uint32), L.dptr(dx), L.dptr(dy))
+            n = len(pix)
+        else:
+            n = rows * cols
+        xyza = np.zeros((n, 4), np.float32)
+        cls = np.zeros(n, np.uint8)
+        status = np.zeros(n, np.uint8)
+        res = RenderResult(xyza, cls, status)
+        a = None
+        if aux:
+            res.xyza64 = np.zeros((n, 4), np.float64)
+            res.steps = np.zeros(n, np.uint32)
+            res.stop_reason = np.zeros(n, np.uint8)
+            a = L.AuxOut(L.dptr(res.xyza64), L.ptr(res.steps, C.c_uint32), L.ptr(res.stop_reason, C.c_uint8))
+        st = L.Stats()
+        L.check(L.lib().grt_render_pixels(self._s, device, row0, col0, rows, cols,
+                                          C.byref(off) if off is not None else None,
+                                          L.ptr(xyza, C.c_float), L.ptr(cls, C.c_uint8), L.ptr(status, C.c_uint8),
+                                          C.byref(a) if a is not None else None, C.byref(st)), "grt_render_pixels")
+        res.stats = _stats_dict(st)
+        return res
+
+    def render_section(self, from_row: int = 0, from_col: int = 0, to_row: Optional[int] = None,
+                       to_col: Optional[int] = None, adaptive: Optional[L.AdaptiveConfig] = None,
+                       sampling_mask_xyza=None, device: int = 0):
+        """render_section_to_cie_buffer (raytracer.rs:177-318): f64 XYZA per pixel."""
+        to_row = self.rows if to_row is None else to_row
+        to_col = self.cols if to_col is None else to_col
+        n = (to_row - from_row) * (to_col - from_col)
+        out = np.zeros((n, 4), np.float64)
+        cls = np.zeros(n, np.uint8)
+        nsel = C.c_uint64(0)
+        st = L.Stats()
+        mask = None
+        if sampling_mask_xyza is not None:
+            mask = np.ascontiguousarray(sampling_mask_xyza, np.float64)
+        L.check(L.lib().grt_render_section(self._s, device, from_row, from_col, to_row, to_col,
+                                           C.byref(adaptive or self.adaptive),
+                                           L.dptr(mask) if mask is not None else None, L.dptr(out),
+                                           L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st)), "grt_render_section")
+        return out, cls, int(nsel.value), _stats_dict(st)
+
+    def color_of_ray(self, row: int, col: int, device: int = 0):
+        """Colour, class and status of one camera pixel (Scene::color_of_ray)."""
+        r = self.render_pixels(row, col, 1, 1, device=device)
+        return r.xyza64[0], int(r.ray_class[0]), int(r.status[0])
+
+
+# --------------------------------------------------------- programmatic scenes ----
+@dataclass
+class Checker:
+    """CheckerMapper (texture.rs:212-257)."""
+    beaming_exponent: float
+    width: float
+    height: float
+    color1: Sequence[int]
+    color2: Sequence[int]
+
+
+@dataclass
+class Bitmap:
+    """TextureMapper (texture.rs:41-102): RGBA8 array (H, W, 4)."""
+    beaming_exponent: float
+    rgba: np.ndarray
+
+
+@dataclass
+class BlackBody:
+    """BlackBodyMapper (texture.rs:104-210)."""
+    beaming_exponent: float = 0.0
+
+
+def srgb_to_xyza(r: int, g: int, b: int, a: int = 255) -> np.ndarray:
+    out = np.zeros(4, np.float64)
+    L.lib().grt_srgb_to_xyza(r, g, b, a, L.dptr(out))
+    return out
+
+
+def r_isco(radius: float, a: float) -> float:
+    return float(L.lib().grt_r_isco(radius, a))
+
+
+def blackbody_xyz(temperature: float, redshift: float = 1.0) -> np.ndarray:
+    out = np.zeros(3, np.float64)
+    L.lib().grt_blackbody_xyz(temperature, redshift, L.dptr(out))
+    return out
+
+
+def kerr_temperature_lut(temperature: float, outer_radius: float, a: float, radius: float, n: int = 1000):
+    lr, lt, ri = np.zeros(n), np.zeros(n), C.c_double(0.0)
+    L.check(L.lib().grt_kerr_temperature_lut(temperature, outer_radius, a, radius, n, L.dptr(lr), L.dptr(lt),
+                                             C.byref(ri)), "KerrTemperatureComputer::new")
+    return lr, lt, float(ri.value)
+
+
+def cartesian_to_spherical(p) -> np.ndarray:
+    i, o = np.ascontiguousarray(p, np.float64), np.zeros(4)
+    L.lib().grt_cartesian_to_spherical(L.dptr(i), L.dptr(o))
+    return o
+
+
+def cartesian_to_boyer_lindquist(a: float, p) -> np.ndarray:
+    i, o = np.ascontiguousarray(p, np.float64), np.zeros(4)
+    L.lib().grt_cartesian_to_boyer_lindquist(a, L.dptr(i), L.dptr(o))
+    return o
+
+
+def build_camera(geometry: int, radius: float, a: float, position, velocity, alpha: float, rows: int, cols: int,
+                 phi: float = 0.0, theta: float = 0.0, psi: float = 0.0) -> L.CameraDesc:
+    """Camera::new (camera.rs:151-196)."""
+    cam = L.CameraDesc()
+    p, v = np.ascontiguousarray(position, np.float64), np.ascontiguousarray(velocity, np.float64)
+    L.check(L.lib().grt_camera_build(geometry, radius, a, L.dptr(p), L.dptr(v), alpha, rows, cols, phi, theta, psi,
+                                     C.byref(cam)), "Camera::new")
+    return cam
+
+
+def stationary_velocity(geometry: int, radius: float, a: float, position) -> np.ndarray:
+    p, o = np.ascontiguousarray(position, np.float64), np.zeros(4)
+    L.lib().grt_stationary_velocity(geometry, radius, a, L.dptr(p), L.dptr(o))
+    return o
+
+
+class SceneBuilder:
+    """Assemble a grt_scene_desc in Python, as the reference tests do with
+    `create_scene_with_camera` (scene.rs:281-369)."""
+
+    def __init__(self, geometry: int, radius: float = 0.0, a: float = 0.0, horizon_epsilon: float = 0.0):
+        self.d = L.SceneDesc()
+        self.d.abi_version = L.GRT_ABI_VERSION
+        self.d.geometry, self.d.radius, self.d.a, self.d.horizon_epsilon = geometry, radius, a, horizon_epsilon
+        self.d.object_hit_opacity_threshold = 0.5
+        self._fill_srgb()
+        self._keep = []
+        self._need_bb = False
+
+    def _fill_srgb(self):
+        # inv_compand_srgb (color.rs:301-308) of each 8-bit code; math.pow is the C libm pow
+        for i in range(256):
+            u = i / 255.0
+            self.d.srgb_to_linear[i] = u / 12.92 if u <= 0.04045 else math.pow((u + 0.055) / 1.055, 2.4)
+
+    def integration(self, max_steps: int, max_radius: float, step_size: float, epsilon: float) -> "SceneBuilder":
+        self.d.max_steps, self.d.max_radius, self.d.step_size, self.d.epsilon = max_steps, max_radius, step_size, epsilon
+        return self
+
+    def camera(self, position, velocity, alpha: float, rows: int, cols: int, phi=0.0, theta=0.0, psi=0.0):
+        self.d.camera = build_camera(self.d.geometry, self.d.radius, self.d.a, position, velocity, alpha, rows, cols,
+                                     phi, theta, psi)
+        return self
+
+    def _texture(self, t) -> L.TextureDesc:
+        d = L.TextureDesc()
+        d.beaming_exponent = t.beaming_exponent
+        if isinstance(t, Checker):
+            d.kind = L.TEX_CHECKER
+            d.checker_width, d.checker_height = t.width, t.height
+            c1, c2 = srgb_to_xyza(*t.color1, 255), srgb_to_xyza(*t.color2, 255)
+            c1[3] = c2[3] = 1.0
+            for k in range(4):
+                d.c1[k], d.c2[k] = c1[k], c2[k]
+        elif isinstance(t, Bitmap):
+            arr = np.ascontiguousarray(t.rgba, np.uint8)
+            assert arr.ndim == 3 and arr.shape[2] == 4
+            self._keep.append(arr)
+            d.kind = L.TEX_BITMAP
+            d.rgba = L.ptr(arr, C.c_uint8)
+            d.height, d.width = arr.shape[0], arr.shape[1]
+        else:
+            d.kind = L.TEX_BLACKBODY
+            self._need_bb = True
+        return d
+
+    def celestial(self, texture, temperature: float = 0.0) -> "SceneBuilder":
+        self.d.celestial = self._texture(texture)
+        self.d.celestial_temperature = temperature
+        return self
+
+    def add_sphere(self, radius: float, center, texture, temperature: float = 0.0) -> "SceneBuilder":
+        o = self.d.objects[self.d.n_objects]
+        o.kind, o.radius, o.temperature = L.OBJ_SPHERE, radius, temperature
+        for k in range(3):
+            o.center[k] = center[k]
+        o.texture = self._texture(texture)
+        self.d.n_objects += 1
+        return self
+
+    def add_disc(self, inner_radius: float, outer_radius: float, texture, temperature: float = 0.0,
+                 constant_temperature: Optional[bool] = None) -> "SceneBuilder":
+        """Disc with geometry.get_temperature_computer(temperature, inner, outer)."""
+        o = self.d.objects[self.d.n_objects]
+        o.kind, o.inner_radius, o.outer_radius = L.OBJ_DISC, inner_radius, outer_radius
+        const = self.d.geometry == L.GEOM_EUCLIDEAN if constant_temperature is None else constant_temperature
+        if const:
+            o.temp_kind, o.temp_constant = L.TEMP_CONSTANT, temperature
+        else:
+            spin = 0.0 if self.d.geometry == L.GEOM_SCHWARZSCHILD else self.d.a
+            lr, lt, ri = kerr_temperature_lut(temperature, outer_radius, spin, self.d.radius)
+            self._keep += [lr, lt]
+            o.temp_kind, o.r_isco, o.lut_n = L.TEMP_KERR_LUT, ri, len(lr)
+            o.lut_r, o.lut_t = L.dptr(lr), L.dptr(lt)
+        o.texture = self._texture(texture)
+        self.d.n_objects += 1
+        return self
+
+    def build(self) -> L.SceneDesc:
+        if self._need_bb and not self.d.bb_n:
+            lt, xyz = np.zeros(1000), np.zeros(3000)
+            L.check(L.lib().grt_blackbody_lut(1000, L.dptr(lt), L.dptr(xyz)), "BlackBodyMapper::new")
+            self._keep += [lt, xyz]
+            self.d.bb_log_t, self.d.bb_xyz, self.d.bb_n = L.dptr(lt), L.dptr(xyz), 1000
+        self.d._keepalive = self._keep  # type: ignore[attr-defined]
+        return self.d
+
+    def scene(self) -> Scene:
+        d = self.build()
+        return Scene(C.pointer(d), keepalive=(self, d))

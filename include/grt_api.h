@@ -1,0 +1,313 @@
+/*
+ * grt_api.h — C ABI of the MI355X-native geodesic ray tracer (gr_raytracer_amd).
+ *
+ * This is the drop-in boundary for the hot path of mdreem/gr_raytracer:
+ *
+ *   Raytracer::render_section_to_cie_buffer_raw   (src/rendering/raytracer.rs:195-244)
+ *   Raytracer::supersample                         (src/rendering/raytracer.rs:320-384)
+ *     -> Scene::color_of_ray                       (src/rendering/scene.rs:114-220)
+ *        -> Integrator::integrate / rkf45          (src/rendering/integrator.rs:78-268,
+ *                                                   src/rendering/runge_kutta.rs:86-182)
+ *        -> Objects::intersects (Sphere / Disc)    (src/scene_objects/objects.rs:65-120)
+ *        -> redshift / texture / blend shade       (src/rendering/{redshift,texture,color}.rs)
+ *
+ * The reference binds these through Rust traits (`RenderableGeometry`, `Geometry`,
+ * `GeodesicSolver`, `Hittable`, `TextureMap`, `TemperatureComputer`); see
+ * src/geometry/geometry.rs:15-153.  Here the scene is flattened to a plain-old-data
+ * descriptor (grt_scene_desc) built once per frame on the host (camera tetrad and
+ * look-up tables included, exactly like `create_scene`, src/cli/shared.rs:131-321),
+ * and the per-pixel work runs in hand-written HIP kernels for gfx950.
+ *
+ * All signatures use plain C types only.  Every function returns 0 on success or a
+ * negative errno-style code; grt_last_error() returns the text of the last failure
+ * on the calling thread.
+ */
+#ifndef GRT_API_H
+#define GRT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GRT_ABI_VERSION 1
+
+/* ---- enums (values are part of the ABI) -------------------------------------- */
+
+/* configuration.rs:111-129 GeometryType (EuclideanSpherical is out of scope). */
+enum grt_geometry_kind {
+  GRT_GEOM_EUCLIDEAN = 0,     /* geometry/euclidean.rs, Cartesian chart, (+,-,-,-)   */
+  GRT_GEOM_SCHWARZSCHILD = 1, /* geometry/schwarzschild.rs, spherical chart, (+,-,-,-) */
+  GRT_GEOM_KERR = 2,          /* geometry/kerr.rs, Kerr-Schild Cartesian, (-,+,+,+)   */
+  GRT_GEOM_KERR_BL = 3        /* geometry/kerr_bl.rs, Boyer-Lindquist, (-,+,+,+)      */
+};
+
+/* configuration.rs:162-177 TextureConfig. */
+enum grt_texture_kind {
+  GRT_TEX_BITMAP = 0,   /* texture.rs:41-102  TextureMapper (bilinear)           */
+  GRT_TEX_CHECKER = 1,  /* texture.rs:212-257 CheckerMapper                      */
+  GRT_TEX_BLACKBODY = 2 /* texture.rs:104-210 BlackBodyMapper (LUT over log10 T) */
+};
+
+/* configuration.rs:188-219 ObjectsConfig (VolumetricDisc is out of scope). */
+enum grt_object_kind {
+  GRT_OBJ_SPHERE = 0, /* scene_objects/sphere.rs */
+  GRT_OBJ_DISC = 1    /* scene_objects/disc.rs   */
+};
+
+/* rendering/temperature.rs: ConstantTemperatureComputer / KerrTemperatureComputer. */
+enum grt_temperature_kind {
+  GRT_TEMP_CONSTANT = 0,
+  GRT_TEMP_KERR_LUT = 1
+};
+
+/* scene.rs:25-30 RayClass. */
+enum grt_ray_class { GRT_CLASS_ESCAPED = 0, GRT_CLASS_CAPTURED = 1, GRT_CLASS_HIT = 2 };
+
+/* Per-pixel status: which RaytracerError (raytracer.rs:20-52) aborted the pixel.
+ * A pixel with a non-zero status keeps the reference default {(0,0,0,1), Escaped}
+ * (raytracer.rs:204-210, :232-239).  Bit 7 flags are informational. */
+enum grt_status {
+  GRT_OK = 0,
+  GRT_ERR_MAX_STEPS_REACHED = 1,     /* runge_kutta.rs:179-181 (100 retries)           */
+  GRT_ERR_NO_CIRCULAR_ORBIT = 2,     /* circular_orbit.rs:93-101                        */
+  GRT_ERR_BELOW_RISCO = 3,           /* temperature.rs:204-217                          */
+  GRT_ERR_NON_FINITE_RADIUS = 4,     /* temperature.rs:199-202                          */
+  GRT_FLAG_HIT_OVERFLOW = 0x80       /* more than GRT_MAX_HITS intersections on one ray */
+};
+
+/* Stop reason of the integration (integrator.rs:22-27), recorded per pixel. */
+enum grt_stop_reason {
+  GRT_STOP_NONE = 0, /* step budget exhausted, no terminal event */
+  GRT_STOP_HORIZON = 1,
+  GRT_STOP_CELESTIAL = 2,
+  GRT_STOP_NAN = 3,
+  GRT_STOP_CLOSED_ORBIT = 4
+};
+
+#define GRT_MAX_OBJECTS 8
+#define GRT_MAX_HITS 16
+
+/* ---- POD scene descriptor ------------------------------------------------------ */
+
+typedef struct grt_texture_desc {
+  int32_t kind;            /* grt_texture_kind */
+  int32_t _pad;
+  double beaming_exponent; /* apply_beaming exponent (color.rs:72-80)              */
+  /* GRT_TEX_BITMAP: caller-owned RGBA8 texels, row-major, width*height*4 bytes.    */
+  const uint8_t* rgba;
+  uint32_t width, height;
+  /* GRT_TEX_CHECKER: cell counts and the two colours already in CIE XYZA          */
+  double checker_width, checker_height;
+  double c1[4], c2[4];
+} grt_texture_desc;
+
+typedef struct grt_object_desc {
+  int32_t kind;          /* grt_object_kind */
+  int32_t temp_kind;     /* grt_temperature_kind (Disc only)                       */
+  /* Sphere: radius, Cartesian centre, constant temperature (sphere.rs:14-35).     */
+  double radius;
+  double center[3];
+  double temperature;
+  /* Disc: annulus in the z = 0 plane (disc.rs:335-356).                            */
+  double inner_radius, outer_radius;
+  /* Disc temperature model: constant, or the KerrTemperatureComputer LUT
+   * (temperature.rs:29-118): r_isco, and n (r, T) pairs strictly increasing in r. */
+  double temp_constant;
+  double r_isco;
+  const double* lut_r;
+  const double* lut_t;
+  uint32_t lut_n;
+  uint32_t _pad2;
+  grt_texture_desc texture;
+} grt_object_desc;
+
+/* The camera after Camera::new (camera.rs:151-196): position and velocity in the
+ * geometry's native chart, the rotated + Lorentz-boosted tetrad rows t, x, y, z,
+ * and the scalars used by get_direction_for (camera.rs:214-232). */
+typedef struct grt_camera_desc {
+  double position[4];
+  double velocity[4];
+  double tetrad[4][4];       /* tetrad[0]=e_t, [1]=e_x, [2]=e_y, [3]=e_z (components) */
+  double alpha;              /* vertical field of view (pi/4 for the CLI, shared.rs:162) */
+  double tan_half_alpha;     /* tan(alpha/2), host libm                                  */
+  int64_t rows, cols;
+  double spatial_signature;  /* signature[3]                                             */
+  double spatial_handedness; /* camera.rs:134-148                                        */
+  /* sin/cos of the camera's polar angle (position[2]) for the spherical and BL charts,
+   * evaluated once on the host (libm) like every other per-frame constant.            */
+  double sin_theta, cos_theta;
+} grt_camera_desc;
+
+typedef struct grt_scene_desc {
+  uint32_t abi_version;      /* = GRT_ABI_VERSION */
+  int32_t geometry;          /* grt_geometry_kind */
+  double radius;             /* r_s (Schwarzschild radius)                      */
+  double a;                  /* spin parameter (Kerr, KerrBL)                   */
+  double horizon_epsilon;
+  /* IntegrationConfiguration (integrator.rs:46-67), from GlobalOpts (cli.rs:5-47). */
+  uint64_t max_steps;
+  double max_radius;
+  double step_size;
+  double epsilon;
+  grt_camera_desc camera;
+  grt_texture_desc celestial;
+  double celestial_temperature;
+  uint32_t n_objects;        /* <= GRT_MAX_OBJECTS, tested in config order     */
+  uint32_t _pad;
+  grt_object_desc objects[GRT_MAX_OBJECTS];
+  /* BlackBodyMapper LUT (texture.rs:120-138): n entries of (log10 T, X, Y, Z).    */
+  const double* bb_log_t;
+  const double* bb_xyz;      /* 3*n, interleaved X,Y,Z                          */
+  uint32_t bb_n;
+  uint32_t _pad3;
+  /* Inverse sRGB companding (color.rs:301-308) of the 256 8-bit codes.            */
+  double srgb_to_linear[256];
+  /* AdaptiveSamplingConfig.object_hit_opacity_threshold (configuration.rs:36).    */
+  double object_hit_opacity_threshold;
+} grt_scene_desc;
+
+/* ---- host-side scene setup (the Rust host's create_scene, cli/shared.rs) -------- */
+
+/* GlobalOpts (cli.rs:5-47). */
+typedef struct grt_global_opts {
+  int64_t width, height;
+  double step_size;
+  uint64_t max_steps;
+  double max_radius;
+  double epsilon;
+  double camera_position[3];
+  double phi, theta, psi;
+  int32_t tone_mapping;       /* 0 Reinhard, 1 GlobalLinear (color.rs:16-21) */
+  int32_t show_sampling_mask;
+  uint8_t sampling_mask_color[3];
+  uint8_t _pad[5];
+} grt_global_opts;
+
+/* AdaptiveSamplingConfig (configuration.rs:21-94). */
+typedef struct grt_adaptive_config {
+  int32_t enabled;
+  uint32_t samples_per_axis;
+  double luminance_contrast_threshold;
+  double opacity_contrast_threshold;
+  int32_t has_minimum_luminance;
+  int32_t exclude_background_contrast;
+  double minimum_luminance;
+  double object_hit_opacity_threshold;
+} grt_adaptive_config;
+
+typedef struct grt_host_scene grt_host_scene; /* owns textures + LUTs + desc */
+
+void grt_default_global_opts(grt_global_opts* opts);
+void grt_default_adaptive_config(grt_adaptive_config* cfg);
+
+/* Parse a scene TOML (configuration.rs schema) and build the frame exactly like
+ * `main.rs:80-116` + `cli/<geometry>.rs::create_scene_internal` + `create_scene`.
+ * Texture paths are resolved relative to `resource_root` (NULL = cwd). */
+int grt_host_scene_load(const char* toml_path, const char* resource_root,
+                        const grt_global_opts* opts, grt_host_scene** out);
+const grt_scene_desc* grt_host_scene_desc(const grt_host_scene* s);
+void grt_host_scene_adaptive(const grt_host_scene* s, grt_adaptive_config* out);
+int grt_host_scene_destroy(grt_host_scene* s);
+
+/* Camera::new (camera.rs:151-196) for an explicit position/velocity in the native
+ * chart of `geometry` (radius, a as in grt_scene_desc).  Fails with -EDOM when a
+ * tetrad is not orthonormal (TetradValidator, tetrad.rs:60-131). */
+int grt_camera_build(int32_t geometry, double radius, double a,
+                     const double position[4], const double velocity[4], double alpha,
+                     int64_t rows, int64_t cols, double phi, double theta, double psi,
+                     grt_camera_desc* out);
+
+/* Per-geometry support quantities used by the host to place the camera. */
+int grt_stationary_velocity(int32_t geometry, double radius, double a,
+                            const double position[4], double out[4]);
+int grt_zamo_velocity(int32_t geometry, double radius, double a,
+                      const double position[4], double out[4]);
+/* Chart conversions (spherical_coordinates_helper.rs:5-61). */
+void grt_cartesian_to_spherical(const double in[4], double out[4]);
+void grt_cartesian_to_boyer_lindquist(double a, const double in[4], double out[4]);
+
+/* KerrTemperatureComputer::new (temperature.rs:45-118): fills n (r, T) pairs.
+ * Returns -ERANGE on DenominatorCloseToZero / NoCircularOrbitPossible. */
+int grt_kerr_temperature_lut(double temperature, double outer_radius, double a,
+                             double radius, uint32_t n, double* lut_r, double* lut_t,
+                             double* r_isco);
+double grt_r_isco(double radius, double a);
+/* BlackBodyMapper::new (texture.rs:121-138): n entries of (log10 T, XYZ). */
+int grt_blackbody_lut(uint32_t n, double* log_t, double* xyz);
+/* integrate_blackbody_xyz (black_body_radiation.rs:18-41). */
+void grt_blackbody_xyz(double temperature, double redshift, double out_xyz[3]);
+/* srgb_to_xyz (color.rs:310-332), alpha := a/255 (CIETristimulus::from_color). */
+void grt_srgb_to_xyza(uint8_t r, uint8_t g, uint8_t b, uint8_t a, double out[4]);
+/* xyz -> tone-mapped sRGB8 (color.rs:204-298), whole buffer. */
+int grt_xyz_to_srgb8(const double* xyza, size_t n, int32_t tone_mapping, double exposure,
+                     uint8_t* rgb_out);
+
+/* ---- device hot path -------------------------------------------------------- */
+
+typedef struct grt_scene grt_scene; /* device-resident copy, one per GPU on demand */
+
+typedef struct grt_stats {
+  uint64_t accepted_steps; /* iterations of integrator.rs:100 that produced a step     */
+  uint64_t attempts;       /* rkf45_step evaluations (6 RHS each)                      */
+  uint64_t rays;
+  uint64_t hit_overflows;
+  double kernel_ms;        /* hipEvent time of the integration kernel(s)               */
+} grt_stats;
+
+/* Optional per-sample sub-pixel offsets (get_ray_for_offset, camera.rs:247-254):
+ * sample k traces pixel (row0 + pix[k] / cols, col0 + pix[k] % cols) at (dx[k], dy[k]). */
+typedef struct grt_offsets {
+  uint64_t count;
+  const uint32_t* pixel_index;
+  const double* dx;
+  const double* dy;
+} grt_offsets;
+
+/* Optional extra per-sample outputs for parity work (any pointer may be NULL). */
+typedef struct grt_aux_out {
+  double* xyza64;       /* 4 doubles per sample: the f64 colour before the f32 cast   */
+  uint32_t* steps;      /* accepted steps per sample                                  */
+  uint8_t* stop_reason; /* grt_stop_reason per sample                                 */
+} grt_aux_out;
+
+int grt_scene_create(const grt_scene_desc* desc, grt_scene** out);
+int grt_scene_destroy(grt_scene* scene);
+const char* grt_last_error(void);
+int grt_device_count(void);
+
+/* Trace a rows x cols rectangle at 1 spp (or the offset list) on `device`.
+ * Host output arrays, row-major over the rectangle (or per offset entry). */
+int grt_render_pixels(grt_scene* scene, int device, uint32_t row0, uint32_t col0,
+                      uint32_t rows, uint32_t cols, const grt_offsets* offsets,
+                      float* xyza_out, uint8_t* class_out, uint8_t* status_out,
+                      const grt_aux_out* aux, grt_stats* stats);
+
+/* Same, but every output pointer is a DEVICE pointer on `device` and the work is
+ * enqueued on `stream` (a hipStream_t, NULL = default stream) without a host sync.
+ * `device_stats` is a device buffer of 4 uint64 counters (accepted, attempts, rays,
+ * overflows) that the kernel accumulates into (caller zeroes it). */
+int grt_render_pixels_async(grt_scene* scene, int device, void* stream,
+                            uint32_t row0, uint32_t col0, uint32_t rows, uint32_t cols,
+                            float* d_xyza, uint8_t* d_class, uint8_t* d_status,
+                            double* d_xyza64, uint32_t* d_steps, uint8_t* d_stop,
+                            uint64_t* d_stats);
+
+/* Whole section with the reference's adaptive supersampling
+ * (render_section_to_cie_buffer[_supersampled], raytracer.rs:177-318), fully on the
+ * device: 1-spp pass, exact 99th-percentile floor, 8-neighbour selection, 16 jittered
+ * rays per selected pixel, ordered average.  Output: f64 XYZA per pixel. */
+int grt_render_section(grt_scene* scene, int device, uint32_t from_row, uint32_t from_col,
+                       uint32_t to_row, uint32_t to_col, const grt_adaptive_config* cfg,
+                       const double* sampling_mask_xyza, double* xyza_out,
+                       uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats);
+
+/* Kernel launch geometry knobs (persistent grid). 0 = library default. */
+int grt_set_launch_config(int blocks_per_cu, int threads_per_block);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRT_API_H */

@@ -1,0 +1,174 @@
+"""ctypes wrapper of the oracle (oracle/grt_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg to check / time the reference algorithm on the CPU.  The product
+(gr_raytracer_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+SO = HERE / "_build" / "liboracle.so"
+_lib = None
+
+_d, _pd = C.c_double, C.POINTER(C.c_double)
+_u8p, _u32p, _u64p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not SO.exists():
+            build()
+        L = C.CDLL(str(SO))
+        vp = C.c_void_p
+        L.oracle_color_of_ray.argtypes = [vp, C.c_int64, C.c_int64, C.c_int, _d, _d, _pd, _u8p, _u8p, _u8p, _u64p, _u64p]
+        L.oracle_render_pixels.restype = _d
+        L.oracle_render_pixels.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, _u32p,
+                                           _pd, _pd, _u32p, C.c_uint32, _pd, _u8p, _u8p, _u8p, _u32p, C.c_int,
+                                           _u64p, _u64p]
+        L.oracle_render_section.restype = C.c_uint64
+        L.oracle_render_section.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, _pd, _pd, _u8p,
+                                            C.c_int]
+        L.oracle_rk_analytic.argtypes = [_d, _pd, _pd]
+        L.oracle_integrate_ray.restype = C.c_int64
+        L.oracle_integrate_ray.argtypes = [vp, _pd, _pd, _pd, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.oracle_camera_ray.argtypes = [vp, _d, _d, C.c_int, _d, _d, _pd]
+        L.oracle_camera_direction.argtypes = [vp, _d, _d, _pd]
+        L.oracle_inner_product.restype = _d
+        L.oracle_inner_product.argtypes = [vp, _pd, _pd, _pd]
+        L.oracle_stratified_offset.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64, _pd, _pd]
+        L.oracle_blend.argtypes = [_pd, _pd, _pd]
+        L.oracle_texture_color.argtypes = [vp, C.c_int, _d, _d, _d, _d, _pd]
+        L.oracle_killing_coefficients.argtypes = [_d, _d, _d, _pd, _pd]
+        L.oracle_object_intersects.argtypes = [vp, C.c_int, _pd, _pd, _pd, _pd]
+        _lib = L
+    return _lib
+
+
+def _addr(desc):
+    return C.cast(C.pointer(desc), C.c_void_p) if not isinstance(desc, C.c_void_p) else desc
+
+
+def _dp(a):
+    return a.ctypes.data_as(_pd)
+
+
+def color_of_ray(desc, row, col, offset=None):
+    xyza = np.zeros(4)
+    cls, status, stop = C.c_uint8(), C.c_uint8(), C.c_uint8()
+    steps, att = C.c_uint64(), C.c_uint64()
+    use, dx, dy = (0, 0.0, 0.0) if offset is None else (1, offset[0], offset[1])
+    lib().oracle_color_of_ray(_addr(desc), row, col, use, dx, dy, _dp(xyza), C.byref(cls), C.byref(status),
+                              C.byref(stop), C.byref(steps), C.byref(att))
+    return {"xyza": xyza, "ray_class": cls.value, "status": status.value, "stop": stop.value,
+            "steps": steps.value, "attempts": att.value}
+
+
+def render_pixels(desc, row0, col0, rows, cols, threads=8, offsets=None, row_list=None):
+    """Returns dict with xyza (n,4) f64, ray_class, status, stop, steps, wall_s, accepted, attempts."""
+    if offsets is not None:
+        pix = np.ascontiguousarray(offsets[0], np.uint32)
+        dx = np.ascontiguousarray(offsets[1], np.float64)
+        dy = np.ascontiguousarray(offsets[2], np.float64)
+        n = len(pix)
+        args = (n, pix.ctypes.data_as(_u32p), _dp(dx), _dp(dy))
+    else:
+        n = rows * cols if row_list is None else len(row_list) * cols
+        args = (0, None, None, None)
+    rl = None if row_list is None else np.ascontiguousarray(row_list, np.uint32)
+    xyza = np.zeros((n, 4))
+    cls, st, stop = np.zeros(n, np.uint8), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+    steps = np.zeros(n, np.uint32)
+    acc, att = C.c_uint64(), C.c_uint64()
+    wall = lib().oracle_render_pixels(_addr(desc), row0, col0, rows, cols, *args,
+                                      rl.ctypes.data_as(_u32p) if rl is not None else None,
+                                      0 if rl is None else len(rl), _dp(xyza), cls.ctypes.data_as(_u8p),
+                                      st.ctypes.data_as(_u8p), stop.ctypes.data_as(_u8p), steps.ctypes.data_as(_u32p),
+                                      threads, C.byref(acc), C.byref(att))
+    return {"xyza": xyza, "ray_class": cls, "status": st, "stop": stop, "steps": steps, "wall_s": wall,
+            "accepted": acc.value, "attempts": att.value}
+
+
+def render_section(desc, from_row, from_col, to_row, to_col, adaptive, mask=None, threads=8):
+    n = (to_row - from_row) * (to_col - from_col)
+    out = np.zeros((n, 4))
+    cls = np.zeros(n, np.uint8)
+    m = None if mask is None else np.ascontiguousarray(mask, np.float64)
+    nsel = lib().oracle_render_section(_addr(desc), from_row, from_col, to_row, to_col,
+                                       C.cast(C.pointer(adaptive), C.c_void_p), _dp(m) if m is not None else None,
+                                       _dp(out), cls.ctypes.data_as(_u8p), threads)
+    return out, cls, int(nsel)
+
+
+def rk_analytic(t_end):
+    y, t = np.zeros(2), C.c_double()
+    lib().oracle_rk_analytic(t_end, _dp(y), C.byref(t))
+    return y, t.value
+
+
+def integrate_ray(desc, position, momentum, max_out=200000):
+    pos, mom = np.ascontiguousarray(position, np.float64), np.ascontiguousarray(momentum, np.float64)
+    out = np.zeros((max_out, 9))
+    stop, status = C.c_int32(), C.c_int32()
+    n = lib().oracle_integrate_ray(_addr(desc), _dp(pos), _dp(mom), _dp(out), max_out, C.byref(stop), C.byref(status))
+    return out[: min(n, max_out)], stop.value, status.value
+
+
+def camera_ray(desc, row, col, offset=None):
+    m = np.zeros(4)
+    use, dx, dy = (0, 0.0, 0.0) if offset is None else (1, offset[0], offset[1])
+    lib().oracle_camera_ray(_addr(desc), float(row), float(col), use, dx, dy, _dp(m))
+    return m
+
+
+def camera_direction(desc, row, col):
+    m = np.zeros(4)
+    lib().oracle_camera_direction(_addr(desc), float(row), float(col), _dp(m))
+    return m
+
+
+def inner_product(desc, position, v, w):
+    p, a, b = (np.ascontiguousarray(x, np.float64) for x in (position, v, w))
+    return lib().oracle_inner_product(_addr(desc), _dp(p), _dp(a), _dp(b))
+
+
+def stratified_offset(row, col, sr, sc, n):
+    dx, dy = C.c_double(), C.c_double()
+    lib().oracle_stratified_offset(row, col, sr, sc, n, C.byref(dx), C.byref(dy))
+    return dx.value, dy.value
+
+
+def blend(self_c, other):
+    a, b, o = np.ascontiguousarray(self_c, np.float64), np.ascontiguousarray(other, np.float64), np.zeros(4)
+    lib().oracle_blend(_dp(a), _dp(b), _dp(o))
+    return o
+
+
+def texture_color(desc, obj, u, v, redshift, temperature):
+    o = np.zeros(4)
+    lib().oracle_texture_color(_addr(desc), obj, u, v, redshift, temperature, _dp(o))
+    return o
+
+
+def killing_coefficients(r_s, a, r):
+    ut, up = C.c_double(), C.c_double()
+    rc = lib().oracle_killing_coefficients(r_s, a, r, C.byref(ut), C.byref(up))
+    return rc, ut.value, up.value
+
+
+def object_intersects(desc, obj, a, b):
+    pa, pb = np.ascontiguousarray(a, np.float64), np.ascontiguousarray(b, np.float64)
+    pt, t = np.zeros(4), C.c_double()
+    hit = lib().oracle_object_intersects(_addr(desc), obj, _dp(pa), _dp(pb), _dp(pt), C.byref(t))
+    return bool(hit), pt, t.value
