@@ -10,7 +10,7 @@ import os
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "lib" / "libgrt.so"
+LIB_PATH = Path(os.environ.get("GRT_LIB", str(PKG_DIR / "lib" / "libgrt.so")))
 
 GRT_ABI_VERSION = 1
 GRT_MAX_OBJECTS = 8

@@ -18,7 +18,7 @@
 #include <string>
 #include <vector>
 
-#include "../../../include/grt_api.h"
+#include "grt_api.h"
 
 namespace grt_host {
 bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err);

@@ -13,7 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../../include/grt_api.h"
+#include "grt_api.h"
 #include "kernels.h"
 
 namespace grt {

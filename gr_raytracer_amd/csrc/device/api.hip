@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "../../../include/grt_api.h"
+#include "grt_api.h"
 #include "../host/host_internal.h"
 #include "dev_scene.h"
 #include "kernels.h"
@@ -51,7 +51,50 @@ struct DeviceCopy {
   int blocks = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // calls on one device are serialised
+  // integrate -> shade hand-off buffers, grown on demand (bytes per ray: ~1.1 KB)
+  uint64_t ws_cap = 0;
+  void* ws_mem = nullptr;
 };
+
+// Carve a Workspace for n rays out of the device's grow-only arena.
+int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
+  const uint64_t M = GRT_MAX_HITS;
+  const uint64_t per_ray = 8 * 8 + 4 * 8 + 1 + 1 + 1 + 4 + M * (4 + 1 + 4 * 8 + 3 * 8);
+  if (n > dc.ws_cap) {
+    if (dc.ws_mem) {
+      (void)hipDeviceSynchronize();  // earlier async launches may still use the old arena
+      (void)hipFree(dc.ws_mem);
+    }
+    dc.ws_mem = nullptr;
+    uint64_t cap = std::max<uint64_t>(n, 1 << 16);
+    if (hipMalloc(&dc.ws_mem, cap * per_ray + 1024) != hipSuccess) {
+      dc.ws_cap = 0;
+      return fail(-ENOMEM, "cannot allocate the integrate/shade workspace");
+    }
+    dc.ws_cap = cap;
+  }
+  uint64_t cap = dc.ws_cap;
+  char* p = (char*)dc.ws_mem;
+  auto take = [&](uint64_t bytes) {
+    char* r = p;
+    p += (bytes + 255) & ~255ull;
+    return (void*)r;
+  };
+  ws->n = n;
+  ws->y = (double*)take(8 * 8 * cap);
+  ws->rc = (double*)take(4 * 8 * cap);
+  ws->rec_p = (double*)take(4 * M * 8 * cap);
+  ws->rec_pt = (double*)take(3 * M * 8 * cap);
+  ws->steps = (uint32_t*)take(4 * cap);
+  ws->rec_win = (uint32_t*)take(M * 4 * cap);
+  ws->stop = (uint8_t*)take(cap);
+  ws->status = (uint8_t*)take(cap);
+  ws->nrec = (uint8_t*)take(cap);
+  ws->rec_obj = (uint8_t*)take(M * cap);
+  // the kernels index with the launch's n, which must not exceed the carved capacity
+  if (n > cap) return fail(-ENOMEM, "workspace too small");
+  return 0;
+}
 
 }  // namespace
 
@@ -207,7 +250,7 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   int occ = 0;
   void (*kfn)() = nullptr;
   (void)kfn;
-  int bpc = g_blocks_per_cu > 0 ? g_blocks_per_cu : 2;
+  int bpc = g_blocks_per_cu > 0 ? g_blocks_per_cu : 2 * GRT_INTEGRATE_WAVES;
   dc.blocks = dc.cus * bpc;
   HIP_TRY(hipEventCreate(&dc.ev0));
   HIP_TRY(hipEventCreate(&dc.ev1));
@@ -238,7 +281,12 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, const g
   // never launch more lanes than there is work for
   uint64_t max_blocks = (wl.n_items + threads - 1) / threads;
   if ((uint64_t)blocks > max_blocks) blocks = (int)std::max<uint64_t>(1, max_blocks);
-  HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, o, dc.d_counter, d_stats, blocks, threads, stream));
+  uint64_t n_out = wl.pixel_index ? wl.n_items : (uint64_t)wl.rows * wl.cols;
+  grt::Workspace ws;
+  int rc = ensure_workspace(dc, n_out, &ws);
+  if (rc) return rc;
+  HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
+                            stream));
   return 0;
 }
 
@@ -336,6 +384,7 @@ int grt_scene_destroy(grt_scene* s) {
     if (!dc) continue;
     (void)hipSetDevice((int)dev);
     for (void* p : dc->allocations) (void)hipFree(p);
+    if (dc->ws_mem) (void)hipFree(dc->ws_mem);
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
     delete dc;

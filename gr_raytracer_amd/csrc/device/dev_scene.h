@@ -79,6 +79,28 @@ struct WorkList {
   const double* dy;
 };
 
+// Hand-off from the integrate kernel to the shade kernel, structure-of-arrays with
+// n = number of output slots of the launch.  Per ray: final state y[8], the per-ray
+// constants (observer energy, KerrBL E / L_z / Q), stop reason, status, step count
+// and up to GRT_MAX_HITS window candidates (slot-major: slot k of ray i at k*n + i).
+struct Workspace {
+  uint64_t n;
+  double* y;          // [8][n]
+  double* rc;         // [4][n]
+  uint8_t* stop;      // [n]
+  uint8_t* status;    // [n]
+  uint8_t* nrec;      // [n] candidates recorded (saturating at 255)
+  uint32_t* steps;    // [n]
+  uint32_t* rec_win;  // [MAX][n] window (accepted-step) index
+  uint8_t* rec_obj;   // [MAX][n] object index
+  double* rec_p;      // [4][MAX][n] momentum lerped to the hit (objects.rs:27-44)
+  double* rec_pt;     // [3][MAX][n] hit point (sphere-local for spheres)
+};
+
+#ifndef GRT_INTEGRATE_WAVES
+#define GRT_INTEGRATE_WAVES 2  // min waves per SIMD requested for the integrate kernel
+#endif
+
 struct Outputs {
   float* xyza;        // 4 floats per sample
   uint8_t* cls;

@@ -24,7 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../../include/grt_api.h"
+#include "grt_api.h"
 #include "dev_scene.h"
 #include "kernels.h"
 
@@ -625,40 +625,36 @@ GDEV int compute_temperature(const DevObject& o, double radius, double* out) {
   return GRT_OK;
 }
 
+
 // ====================================================== window (chord) tests ======
-struct Hit {
-  double u, v, t;
-  double px, py, pz;  // Cartesian (world) intersection point
-};
+// Geometry only: the integrate kernel decides hit / no hit, the chord parameter t and
+// the hit point; everything that needs the emitter (energy, temperature, colour) is
+// evaluated later by the shade kernel from the recorded point and momentum.
 
 // disc.rs:41-88.  The sign / magnitude pre-filter only skips divisions whose quotient
-// is provably outside [0, 1]; every accepted t is the same correctly-rounded p1/p2.
-GDEV bool disc_hit(const DevObject& o, const double* s, const double* e, Hit* h) {
+// is provably outside [0, 1] (and cannot underflow to -0); every accepted t is the
+// same correctly rounded p1 / p2 the reference computes.
+GDEV bool disc_chord(const DevObject& o, const double* s, const double* e, double* t_out, double* ip) {
   double d0 = e[0] - s[0], d1 = e[1] - s[1], d2 = e[2] - s[2];
   double p1 = (0.0 - s[0]) * 0.0 + (0.0 - s[1]) * 0.0 + (0.0 - s[2]) * 1.0;
   double p2 = d0 * 0.0 + d1 * 0.0 + d2 * 1.0;
-  if ((p1 > 0.0 && p2 < 0.0) || (p1 < 0.0 && p2 > 0.0)) return false;  // t < 0
-  if (fabs(p1) > 2.0 * fabs(p2)) return false;                         // t > 2
+  double a1 = fabs(p1), a2 = fabs(p2);
+  if (a1 > 1e-200 && a2 < 1e100 && ((p1 > 0.0 && p2 < 0.0) || (p1 < 0.0 && p2 > 0.0))) return false;  // t < 0
+  if (a1 > 2.0 * a2) return false;                                                                    // t > 2
   double t = p1 / p2;
   if (!(0.0 <= t && t <= 1.0)) return false;
   double ix = s[0] + t * d0, iy = s[1] + t * d1, iz = s[2] + t * d2;
   double rr = ix * ix + iy * iy + iz * iz;
   if (!(rr >= o.rin2 && rr <= o.rout2)) return false;
-  double phi = atan2(iy - 0.0, ix - 0.0);
-  double r = (sqrt(rr) - o.rin) / (o.rout - o.rin);
-  double sp, cp;
-  sincos(phi, &sp, &cp);
-  h->u = 0.5 + 0.5 * r * cp;
-  h->v = 0.5 + 0.5 * r * sp;
-  h->t = t;
-  h->px = ix;
-  h->py = iy;
-  h->pz = iz;
+  *t_out = t;
+  ip[0] = ix;
+  ip[1] = iy;
+  ip[2] = iz;
   return true;
 }
 
-// sphere.rs:37-128
-GDEV bool sphere_hit(const DevObject& o, const double* s_w, const double* e_w, Hit* h) {
+// sphere.rs:37-128; returns the hit point in the sphere's local frame.
+GDEV bool sphere_chord(const DevObject& o, const double* s_w, const double* e_w, double* t_out, double* lp) {
   double s0 = s_w[0] + -o.cx, s1 = s_w[1] + -o.cy, s2 = s_w[2] + -o.cz;
   double e0 = e_w[0] + -o.cx, e1 = e_w[1] + -o.cy, e2 = e_w[2] + -o.cz;
   double r_start = s0 * s0 + s1 * s1 + s2 * s2;
@@ -678,105 +674,14 @@ GDEV bool sphere_hit(const DevObject& o, const double* s_w, const double* e_w, H
   if (0.0 <= t1 && t1 <= 1.0) t = t1;
   else if (0.0 <= t2 && t2 <= 1.0) t = t2;
   else return false;
-  double px = s0 + t * d0, py = s1 + t * d1, pz = s2 + t * d2;
-  double rr, theta, phi;
-  cart_to_sph(px, py, pz, &rr, &theta, &phi);
-  double u = (PI + phi) / TWO_PI;
-  h->u = 1.0 - u;
-  h->v = theta / PI;
-  h->t = t;
-  h->px = px + o.cx;
-  h->py = py + o.cy;
-  h->pz = pz + o.cz;
+  *t_out = t;
+  lp[0] = s0 + t * d0;
+  lp[1] = s1 + t * d1;
+  lp[2] = s2 + t * d2;
   return true;
 }
 
-// Emitter step at the intersection (objects.rs:27-44 + :95-115) and its colour.
-// Returns a grt_status; on success *col holds the hit colour.
-template <int G>
-GDEV int shade_hit(const DevScene& S, const RayConst& rc, const DevObject& o, const Hit& h,
-                   const double* ys, const double* ye, XYZA* col) {
-  // step.x = intersection point converted to the native chart
-  double x[4];
-  double st, ct;
-  x[0] = 0.0;
-  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
-    cart_to_sph(h.px, h.py, h.pz, &x[1], &x[2], &x[3]);
-    sincos(x[2], &st, &ct);
-  } else if constexpr (G == GRT_GEOM_KERR_BL) {
-    cart_to_bl(S.a, h.px, h.py, h.pz, &x[1], &x[2], &x[3]);
-    sincos(x[2], &st, &ct);
-  } else {
-    x[1] = h.px;
-    x[2] = h.py;
-    x[3] = h.pz;
-    st = 0.0;
-    ct = 0.0;
-  }
-  // step.p = lerp of the window's endpoint momenta
-  double pa[4], pb[4], p[4];
-  momentum<G>(S, rc, ys, pa);
-  momentum<G>(S, rc, ye, pb);
-  double sw = 1.0 - h.t;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) p[i] = sw * pa[i] + h.t * pb[i];
-  double u[4];
-  if (o.kind == GRT_OBJ_DISC) {  // disc.rs:101-110: circular-orbit emitter
-    if constexpr (G == GRT_GEOM_EUCLIDEAN) {
-      u[0] = 1.0; u[1] = 0.0; u[2] = 0.0; u[3] = 0.0;
-    } else {
-      double r;
-      if constexpr (G == GRT_GEOM_KERR) r = sqrt(ks_r_sqr(S.a, x[1], x[2], x[3]));
-      else r = x[1];
-      double ut, uphi;
-      if (!killing_coefficients(S, r, &ut, &uphi)) return GRT_ERR_NO_CIRCULAR_ORBIT;
-      if constexpr (G == GRT_GEOM_KERR) {
-        double ax[4] = {0.0, -x[2], x[1], 0.0};
-        double et[4] = {1.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) u[i] = ut * et[i] + uphi * ax[i];
-      } else {
-        u[0] = ut; u[1] = 0.0; u[2] = 0.0; u[3] = uphi;
-      }
-    }
-  } else {  // sphere.rs:141-150: static emitter
-    stationary_velocity<G>(S, x, ct, u);
-  }
-  double em = inner<G>(S, x, st, ct, u, p);
-  double sig0 = signature0<G>();
-  double redshift = (sig0 * rc.obs) / (sig0 * em);
-  double temperature;
-  if (o.kind == GRT_OBJ_DISC) {
-    double rad;  // get_radial_coordinate of the Cartesian intersection point
-    if constexpr (G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) {
-      rad = sqrt(ks_r_sqr(S.a, h.px, h.py, h.pz));
-    } else {
-      rad = sqrt(h.px * h.px + h.py * h.py + h.pz * h.pz);
-    }
-    int e = compute_temperature(o, rad, &temperature);
-    if (e != GRT_OK) return e;
-  } else {
-    temperature = o.temperature;
-  }
-  *col = texture_color(S, o.tex, h.u, h.v, redshift, temperature);
-  return GRT_OK;
-}
-
-// ============================================================== kernel ==========
-template <int G>
-struct Lane {
-  double y[8], yp[8];
-  double c[3], cp[3];
-  double t, h, h_cur;
-  uint64_t i;
-  int retries;
-  RayConst rc;
-  double opacity;
-  int nhits;
-  int status;
-  uint32_t steps;
-};
-
+// ======================================================== integrate kernel =======
 // camera.rs:214-232 get_direction_for, then momentum = direction - e_t (:243, :252)
 GDEV void camera_momentum(const DevCamera& c, double row, double column, double* p) {
   double shifted_column = column + 1.0;
@@ -794,17 +699,17 @@ GDEV void camera_momentum(const DevCamera& c, double row, double column, double*
   }
 }
 
-// Create the ray state (integrator.rs:82-99 + geometry-specific create_initial_state).
+// Create the ray state (integrator.rs:82-99 + geometry-specific create_initial_state);
+// writes the per-ray constants (observer energy, KerrBL E/L_z/Q) to the workspace.
 template <int G>
-GDEV void init_ray(const DevScene& S, Lane<G>& L, double row, double col) {
+GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayConst& rc) {
   const DevCamera& cam = S.cam;
   double p[4];
   camera_momentum(cam, row, col, p);
-  // observer energy at the camera (redshift.rs:40-43), camera sin/cos from the host
-  L.rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
-  L.rc.e = 0.0;
-  L.rc.lz = 0.0;
-  L.rc.q = 0.0;
+  rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);  // redshift.rs:40-43
+  rc.e = 0.0;
+  rc.lz = 0.0;
+  rc.q = 0.0;
   if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:505-577, :176-223 (BL ray)
     double a = S.a, radius = S.radius;
     double r = cam.pos[1];
@@ -816,9 +721,9 @@ GDEV void init_ray(const DevScene& S, Lane<G>& L, double row, double col) {
     double e = -pc[0], l_z = pc[3], p_theta = pc[2];
     double sin2 = st * st;
     double q = p_theta * p_theta + ct * ct * (l_z * l_z / fmax(sin2, 1e-28) - a * a * e * e);
-    L.rc.e = e;
-    L.rc.lz = l_z;
-    L.rc.q = q;
+    rc.e = e;
+    rc.lz = l_z;
+    rc.q = q;
     double sign_r = p[1] >= 0.0 ? 1.0 : -1.0;
     double sign_theta = p[2] >= 0.0 ? 1.0 : -1.0;
     double del = bl_delta(r, radius, a);
@@ -826,14 +731,14 @@ GDEV void init_ray(const DevScene& S, Lane<G>& L, double row, double col) {
     double le = l_z - a * e;
     double r_pot = p_r * p_r - del * (le * le + q);
     double th_pot = q + a * a * e * e * ct * ct - l_z * l_z * ct * ct / (st * st);
-    L.y[0] = cam.pos[0];
-    L.y[1] = r;
-    L.y[2] = cam.pos[2];
-    L.y[3] = cam.pos[3];
-    L.y[4] = sign_r * sqrt(fmax(r_pot, 0.0));
-    L.y[5] = sign_theta * sqrt(fmax(th_pot, 0.0));
-    L.y[6] = 0.0;
-    L.y[7] = 0.0;
+    y[0] = cam.pos[0];
+    y[1] = r;
+    y[2] = cam.pos[2];
+    y[3] = cam.pos[3];
+    y[4] = sign_r * sqrt(fmax(r_pot, 0.0));
+    y[5] = sign_theta * sqrt(fmax(th_pot, 0.0));
+    y[6] = 0.0;
+    y[7] = 0.0;
   } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:243-260
     double g[4][4];
     ks_metric(S.radius, S.a, cam.pos[1], cam.pos[2], cam.pos[3], g);
@@ -841,26 +746,16 @@ GDEV void init_ray(const DevScene& S, Lane<G>& L, double row, double col) {
     mat_vec(g, p, pc);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      L.y[k] = cam.pos[k];
-      L.y[4 + k] = pc[k];
+      y[k] = cam.pos[k];
+      y[4 + k] = pc[k];
     }
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      L.y[k] = cam.pos[k];
-      L.y[4 + k] = p[k];
+      y[k] = cam.pos[k];
+      y[4 + k] = p[k];
     }
   }
-  L.t = 0.0;
-  L.h = S.step_size;
-  L.h_cur = rclamp(L.h, H_MIN, H_MAX);
-  L.i = 0;
-  L.retries = 0;
-  L.opacity = 0.0;
-  L.nhits = 0;
-  L.status = GRT_OK;
-  L.steps = 0;
-  to_cart<G>(S, L.y, L.c);
 }
 
 // integrator.rs:203-268
@@ -883,76 +778,44 @@ GDEV int should_stop(const DevScene& S, const double* y, const double* c, uint64
   return GRT_STOP_NONE;
 }
 
-// Terminal colour + back-to-front blend (scene.rs:153-219).
-template <int G>
-GDEV XYZA finalize_color(const DevScene& S, const Lane<G>& L, int stop, const XYZA* hits, int* cls) {
-  XYZA result{0.0, 0.0, 0.0, 1.0};
-  *cls = GRT_CLASS_CAPTURED;
-  if (stop == GRT_STOP_HORIZON || stop == GRT_STOP_CLOSED_ORBIT) {
-    result = blend(result, XYZA{0.0, 0.0, 0.0, 1.0});
-  } else if (stop == GRT_STOP_CELESTIAL) {
-    const double* y = L.y;
-    double th, ph;  // get_as_spherical (point.rs:172-188)
-    double st, ct;
-    if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
-      th = rem_euclid(y[2], PI);
-      ph = rem_euclid(y[3] + PI, TWO_PI) - PI;
-      sincos(y[2], &st, &ct);
-    } else {
-      double rr;
-      cart_to_sph(y[1], y[2], y[3], &rr, &th, &ph);
-      st = 0.0;
-      ct = 0.0;
-    }
-    double u = (PI + ph) / TWO_PI;
-    double v = th / PI;
-    double vel[4], p[4];
-    stationary_velocity<G>(S, y, ct, vel);
-    momentum<G>(S, L.rc, y, p);
-    double em = inner<G>(S, y, st, ct, vel, p);
-    double sig0 = signature0<G>();
-    double redshift = (sig0 * L.rc.obs) / (sig0 * em);
-    result = blend(result, texture_color(S, S.celestial, 1.0 - u, v, redshift, S.celestial_temperature));
-    *cls = GRT_CLASS_ESCAPED;
-  }
-  int n = L.nhits < GRT_MAX_HITS ? L.nhits : GRT_MAX_HITS;
-  for (int k = n - 1; k >= 0; --k) result = blend(result, hits[k]);
-  if (L.opacity >= S.hit_threshold) *cls = GRT_CLASS_HIT;
-  return result;
-}
-
-GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, int status, int stop,
+// End of a ray: its final state goes to the workspace for the shade kernel.
+GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, int stop, int status, uint32_t nrec,
                     uint32_t steps) {
-  reinterpret_cast<float4*>(out.xyza)[idx] = make_float4((float)c.x, (float)c.y, (float)c.z, (float)c.a);
-  out.cls[idx] = (uint8_t)cls;
-  out.status[idx] = (uint8_t)status;
-  if (out.xyza64) {
-    double* d = out.xyza64 + 4 * idx;
-    d[0] = c.x;
-    d[1] = c.y;
-    d[2] = c.z;
-    d[3] = c.a;
-  }
-  if (out.steps) out.steps[idx] = steps;
-  if (out.stop) out.stop[idx] = (uint8_t)stop;
+  const uint64_t n = ws.n;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ws.y[k * n + idx] = y[k];
+  ws.stop[idx] = (uint8_t)stop;
+  ws.status[idx] = (uint8_t)status;
+  ws.nrec[idx] = nrec > 255u ? 255u : nrec;
+  ws.steps[idx] = steps;
 }
 
+// One lane integrates one ray at a time: RKF45 attempts, and after every accepted
+// step the chord test of window (previous step, step) against every object in config
+// order (objects.rs:81) and the stop test.  A window hit nearer than the current
+// nearest (objects.rs:86-88) is recorded as a candidate: its object, window index,
+// hit point and the lerped momentum (objects.rs:27-44).
 template <int G>
-__global__ void __launch_bounds__(256) trace_kernel(const DevScene* __restrict__ Sp, WorkList wl,
-                                                    Outputs out,
-                                                    unsigned long long* __restrict__ counter,
-                                                    unsigned long long* __restrict__ stats) {
+__global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
+    const DevScene* __restrict__ Sp, WorkList wl, Workspace ws, unsigned long long* __restrict__ counter,
+    unsigned long long* __restrict__ stats) {
   const DevScene& S = *Sp;
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr uint64_t CHUNK = 64;
+  const uint64_t n = ws.n;
 
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
-  uint64_t out_idx = 0;
-  Lane<G> L;
-  XYZA hits[GRT_MAX_HITS];
-  uint64_t n_acc = 0, n_att = 0, n_rays = 0, n_over = 0;
+  uint64_t idx = 0;      // output slot of the current ray
+  double y[8];           // state
+  double c[3];           // Cartesian position of the last accepted step
+  double h = 0.0, h_cur = 0.0;
+  uint64_t i = 0;        // accepted step index
+  int retries = 0;
+  uint32_t nrec = 0;
+  RayConst rc;
+  uint64_t n_acc = 0, n_att = 0, n_rays = 0;
 
   while (true) {
     // ---------------- lane refill: ballot, one atomic per 64 items --------------
@@ -980,8 +843,8 @@ __global__ void __launch_bounds__(256) trace_kernel(const DevScene* __restrict__
             double r = (double)(wl.row0 + pix / wl.cols), cc = (double)(wl.col0 + pix % wl.cols);
             row = r + (wl.dy[item] - 0.5);
             col = cc + (wl.dx[item] - 0.5);
-            out_idx = item;
-          } else {  // 8x8 pixel tiles, row-major tiles
+            idx = item;
+          } else {  // 8x8 pixel tiles, row-major tiles: a wave starts on a compact patch
             uint64_t tile = item >> 6;
             uint32_t w = (uint32_t)(item & 63);
             uint32_t tr = (uint32_t)(tile / wl.tiles_x), tc = (uint32_t)(tile % wl.tiles_x);
@@ -989,16 +852,24 @@ __global__ void __launch_bounds__(256) trace_kernel(const DevScene* __restrict__
             valid = (r < wl.rows) && (cc < wl.cols);
             row = (double)(wl.row0 + r);
             col = (double)(wl.col0 + cc);
-            out_idx = (uint64_t)r * wl.cols + cc;
+            idx = (uint64_t)r * wl.cols + cc;
           }
           if (valid) {
-            init_ray<G>(S, L, row, col);
+            init_ray<G>(S, row, col, y, rc);
+            ws.rc[0 * n + idx] = rc.obs;
+            ws.rc[1 * n + idx] = rc.e;
+            ws.rc[2 * n + idx] = rc.lz;
+            ws.rc[3 * n + idx] = rc.q;
+            to_cart<G>(S, y, c);
+            h = S.step_size;
+            h_cur = rclamp(h, H_MIN, H_MAX);
+            i = 0;
+            retries = 0;
+            nrec = 0;
             active = true;
             n_rays++;
             if (S.max_steps <= 1) {  // `for i in 1..max_steps` never runs
-              int cls;
-              XYZA col_ = finalize_color<G>(S, L, GRT_STOP_NONE, hits, &cls);
-              write_out(out, out_idx, col_, cls, GRT_OK, GRT_STOP_NONE, 0);
+              store_ray(ws, idx, y, GRT_STOP_NONE, GRT_OK, 0, 0);
               active = false;
             }
           }
@@ -1016,95 +887,77 @@ __global__ void __launch_bounds__(256) trace_kernel(const DevScene* __restrict__
 
     // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
     double yn[8];
-    double err = rkf_attempt<G>(S, L.rc, L.y, L.h_cur, yn);
+    double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
     n_att++;
-    double h_prop = err > 0.0 ? BETA * L.h_cur * pow(S.epsilon / err, INV_ORDER) : L.h_cur * H_GROWTH;
-    h_prop = rclamp(fmin(h_prop, L.h_cur * H_GROWTH), H_MIN, H_MAX);
-    bool accept;
-    double h_next = 0.0;
+    double h_prop = err > 0.0 ? BETA * h_cur * pow(S.epsilon / err, INV_ORDER) : h_cur * H_GROWTH;
+    h_prop = rclamp(fmin(h_prop, h_cur * H_GROWTH), H_MIN, H_MAX);
+    double h_next;
     if (err > S.epsilon) {
-      if (L.h_cur <= H_MIN) {
-        accept = true;
-        h_next = L.h_cur;
+      if (h_cur <= H_MIN) {
+        h_next = h_cur;
       } else {
-        accept = false;
-        L.h_cur = rclamp(h_prop / 2.0, H_MIN, H_MAX);
-        if (++L.retries >= MAX_RETRY) {  // Err(MaxStepsReached)
-          write_out(out, out_idx, XYZA{0.0, 0.0, 0.0, 1.0}, GRT_CLASS_ESCAPED, GRT_ERR_MAX_STEPS_REACHED,
-                    GRT_STOP_NONE, L.steps);
+        h_cur = rclamp(h_prop / 2.0, H_MIN, H_MAX);
+        if (++retries >= MAX_RETRY) {  // Err(MaxStepsReached)
+          store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
           active = false;
-          continue;
         }
+        continue;
       }
     } else {
-      accept = true;
-      h_next = (err / S.epsilon < SMALL_ERR) ? rclamp(L.h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
+      h_next = (err / S.epsilon < SMALL_ERR) ? rclamp(h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
     }
-    if (!accept) continue;
 
     // ---------------- accepted step i (integrator.rs:100-162) --------------------
-    L.t += L.h_cur;
-    L.h = h_next;
-    L.i++;
-    L.steps++;
+    h = h_next;
+    i++;
     n_acc++;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      L.yp[k] = L.y[k];
-      L.y[k] = yn[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) L.cp[k] = L.c[k];
-    to_cart<G>(S, L.y, L.c);
-
-    // window (yp -> y) against every object, nearest hit wins (objects.rs:65-120)
-    int werr = GRT_OK;
-    bool has = false;
-    XYZA wcol;
+    double cn[3];
+    to_cart<G>(S, yn, cn);
+    // window (y -> yn) against every object; record each new nearest candidate
     double shortest = 1.7976931348623157e308;
     for (uint32_t k = 0; k < S.n_objects; ++k) {
       const DevObject& o = S.obj[k];
-      Hit hh;
-      bool hit = (o.kind == GRT_OBJ_DISC) ? disc_hit(o, L.cp, L.c, &hh) : sphere_hit(o, L.cp, L.c, &hh);
+      double t, pt[3];
+      bool hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
       if (!hit) continue;
-      double dx = hh.px - L.cp[0], dy = hh.py - L.cp[1], dz = hh.pz - L.cp[2];
-      double distance = sqrt(dx * dx + dy * dy + dz * dz);
-      if (distance < shortest) {
-        shortest = distance;
-        XYZA cc;
-        int e = shade_hit<G>(S, L.rc, o, hh, L.yp, L.y, &cc);
-        if (e != GRT_OK) {
-          werr = e;
-          break;
-        }
-        wcol = cc;
-        has = true;
+      double wx = pt[0], wy = pt[1], wz = pt[2];
+      if (o.kind != GRT_OBJ_DISC) {
+        wx = pt[0] + o.cx;
+        wy = pt[1] + o.cy;
+        wz = pt[2] + o.cz;
       }
+      double dx = wx - c[0], dy = wy - c[1], dz = wz - c[2];
+      double distance = sqrt(dx * dx + dy * dy + dz * dz);
+      if (!(distance < shortest)) continue;
+      shortest = distance;
+      if (nrec < GRT_MAX_HITS) {
+        double pa[4], pb[4];
+        momentum<G>(S, rc, y, pa);
+        momentum<G>(S, rc, yn, pb);
+        double sw = 1.0 - t;
+        const uint64_t slot = (uint64_t)nrec * n + idx;
+        ws.rec_win[slot] = (uint32_t)i;
+        ws.rec_obj[slot] = (uint8_t)k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
+      }
+      nrec++;
     }
-    if (werr != GRT_OK) {  // any window error aborts the pixel (scene.rs:146)
-      write_out(out, out_idx, XYZA{0.0, 0.0, 0.0, 1.0}, GRT_CLASS_ESCAPED, werr, GRT_STOP_NONE, L.steps);
-      active = false;
-      continue;
-    }
-    if (has) {
-      if (L.nhits < GRT_MAX_HITS) hits[L.nhits] = wcol;
-      else L.status |= GRT_FLAG_HIT_OVERFLOW;
-      L.nhits++;
-      double alpha = rclamp(wcol.a, 0.0, 1.0);
-      L.opacity = alpha + L.opacity * (1.0 - alpha);
-    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = yn[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = cn[k];
 
-    int stop = should_stop<G>(S, L.y, L.c, L.i);
-    if (stop != GRT_STOP_NONE || L.i == S.max_steps - 1) {
-      int cls;
-      XYZA col_ = finalize_color<G>(S, L, stop, hits, &cls);
-      if (L.status & GRT_FLAG_HIT_OVERFLOW) n_over++;
-      write_out(out, out_idx, col_, cls, L.status, stop, L.steps);
+    int stop = should_stop<G>(S, y, c, i);
+    if (stop != GRT_STOP_NONE || i == S.max_steps - 1) {
+      store_ray(ws, idx, y, stop, GRT_OK, nrec, (uint32_t)i);
       active = false;
       continue;
     }
-    L.retries = 0;
-    L.h_cur = rclamp(L.h, H_MIN, H_MAX);
+    retries = 0;
+    h_cur = rclamp(h, H_MIN, H_MAX);
   }
 
   // per-wave reduction of the counters, one atomic per wave
@@ -1113,38 +966,228 @@ __global__ void __launch_bounds__(256) trace_kernel(const DevScene* __restrict__
     n_acc += __shfl_down(n_acc, off);
     n_att += __shfl_down(n_att, off);
     n_rays += __shfl_down(n_rays, off);
-    n_over += __shfl_down(n_over, off);
   }
   if (lane == 0) {
     atomicAdd(stats + 0, (unsigned long long)n_acc);
     atomicAdd(stats + 1, (unsigned long long)n_att);
     atomicAdd(stats + 2, (unsigned long long)n_rays);
-    atomicAdd(stats + 3, (unsigned long long)n_over);
   }
 }
 
+// ============================================================ shade kernel =======
+// Evaluate one recorded candidate: the emitter step at the intersection
+// (objects.rs:27-44 + :95-115), its redshift, temperature and texture colour.
+template <int G>
+GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o, const double* p,
+                      const double* pt, XYZA* col) {
+  double u_tex, v_tex, wx, wy, wz;
+  if (o.kind == GRT_OBJ_DISC) {  // disc.rs:60-76 uv from the in-plane point
+    wx = pt[0];
+    wy = pt[1];
+    wz = pt[2];
+    double rr = wx * wx + wy * wy + wz * wz;
+    double phi = atan2(wy - 0.0, wx - 0.0);
+    double r = (sqrt(rr) - o.rin) / (o.rout - o.rin);
+    double sp, cp;
+    sincos(phi, &sp, &cp);
+    u_tex = 0.5 + 0.5 * r * cp;
+    v_tex = 0.5 + 0.5 * r * sp;
+  } else {  // sphere.rs:92-117 uv from the sphere-local point, world point for physics
+    double rr, theta, phi;
+    cart_to_sph(pt[0], pt[1], pt[2], &rr, &theta, &phi);
+    double u = (PI + phi) / TWO_PI;
+    u_tex = 1.0 - u;
+    v_tex = theta / PI;
+    wx = pt[0] + o.cx;
+    wy = pt[1] + o.cy;
+    wz = pt[2] + o.cz;
+  }
+  double x[4];  // step.x = intersection point converted to the native chart
+  double st = 0.0, ct = 0.0;
+  x[0] = 0.0;
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
+    cart_to_sph(wx, wy, wz, &x[1], &x[2], &x[3]);
+    sincos(x[2], &st, &ct);
+  } else if constexpr (G == GRT_GEOM_KERR_BL) {
+    cart_to_bl(S.a, wx, wy, wz, &x[1], &x[2], &x[3]);
+    sincos(x[2], &st, &ct);
+  } else {
+    x[1] = wx;
+    x[2] = wy;
+    x[3] = wz;
+  }
+  double u[4];
+  if (o.kind == GRT_OBJ_DISC) {  // disc.rs:101-110: circular-orbit emitter
+    if constexpr (G == GRT_GEOM_EUCLIDEAN) {
+      u[0] = 1.0; u[1] = 0.0; u[2] = 0.0; u[3] = 0.0;
+    } else {
+      double r;
+      if constexpr (G == GRT_GEOM_KERR) r = sqrt(ks_r_sqr(S.a, x[1], x[2], x[3]));
+      else r = x[1];
+      double ut, uphi;
+      if (!killing_coefficients(S, r, &ut, &uphi)) return GRT_ERR_NO_CIRCULAR_ORBIT;
+      if constexpr (G == GRT_GEOM_KERR) {
+        double ax[4] = {0.0, -x[2], x[1], 0.0};
+        double et[4] = {1.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u[q] = ut * et[q] + uphi * ax[q];
+      } else {
+        u[0] = ut; u[1] = 0.0; u[2] = 0.0; u[3] = uphi;
+      }
+    }
+  } else {  // sphere.rs:141-150: static emitter
+    stationary_velocity<G>(S, x, ct, u);
+  }
+  double em = inner<G>(S, x, st, ct, u, p);
+  double sig0 = signature0<G>();
+  double redshift = (sig0 * rc.obs) / (sig0 * em);  // redshift.rs:36-38
+  double temperature;
+  if (o.kind == GRT_OBJ_DISC) {
+    double rad;  // get_radial_coordinate of the Cartesian intersection point
+    if constexpr (G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) {
+      rad = sqrt(ks_r_sqr(S.a, wx, wy, wz));
+    } else {
+      rad = sqrt(wx * wx + wy * wy + wz * wz);
+    }
+    int e = compute_temperature(o, rad, &temperature);
+    if (e != GRT_OK) return e;
+  } else {
+    temperature = o.temperature;
+  }
+  *col = texture_color(S, o.tex, u_tex, v_tex, redshift, temperature);
+  return GRT_OK;
+}
+
+GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, int status, int stop,
+                    uint32_t steps) {
+  reinterpret_cast<float4*>(out.xyza)[idx] = make_float4((float)c.x, (float)c.y, (float)c.z, (float)c.a);
+  out.cls[idx] = (uint8_t)cls;
+  out.status[idx] = (uint8_t)status;
+  if (out.xyza64) {
+    double* d = out.xyza64 + 4 * idx;
+    d[0] = c.x;
+    d[1] = c.y;
+    d[2] = c.z;
+    d[3] = c.a;
+  }
+  if (out.steps) out.steps[idx] = steps;
+  if (out.stop) out.stop[idx] = (uint8_t)stop;
+}
+
+// Scene::color_of_ray's window pass, terminal colour and composite (scene.rs:141-219),
+// one lane per ray, over the candidates the integrate kernel recorded.
+template <int G>
+__global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__ Sp, Workspace ws, Outputs out,
+                                                    unsigned long long* __restrict__ stats) {
+  const DevScene& S = *Sp;
+  const uint64_t n = ws.n;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  int status = ws.status[idx];
+  int stop = ws.stop[idx];
+  uint32_t steps = ws.steps[idx];
+  const XYZA fail{0.0, 0.0, 0.0, 1.0};
+  if (status != GRT_OK) {  // integrate error: reference default pixel (raytracer.rs:204-210)
+    write_out(out, idx, fail, GRT_CLASS_ESCAPED, status, stop, steps);
+    return;
+  }
+  RayConst rc{ws.rc[idx], ws.rc[n + idx], ws.rc[2 * n + idx], ws.rc[3 * n + idx]};
+  uint32_t nrec = ws.nrec[idx];
+  uint32_t nr = nrec < GRT_MAX_HITS ? nrec : GRT_MAX_HITS;
+  XYZA hits[GRT_MAX_HITS];
+  int nh = 0;
+  double opacity = 0.0;
+  for (uint32_t j = 0; j < nr; ++j) {
+    const uint64_t slot = (uint64_t)j * n + idx;
+    uint32_t win = ws.rec_win[slot];
+    const DevObject& o = S.obj[ws.rec_obj[slot]];
+    double p[4], pt[3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot];
+    XYZA col;
+    int e = shade_record<G>(S, rc, o, p, pt, &col);
+    if (e != GRT_OK) {  // any window error aborts the pixel (scene.rs:146, objects.rs:96-102)
+      write_out(out, idx, fail, GRT_CLASS_ESCAPED, e, stop, steps);
+      return;
+    }
+    bool last_in_window = (j + 1 == nr) || (ws.rec_win[slot + n] != win);
+    if (last_in_window) {  // the window's nearest hit
+      hits[nh++] = col;
+      double alpha = rclamp(col.a, 0.0, 1.0);
+      opacity = alpha + opacity * (1.0 - alpha);
+    }
+  }
+  // terminal colour (scene.rs:157-205) and back-to-front blend (:206-210)
+  XYZA result{0.0, 0.0, 0.0, 1.0};
+  int cls = GRT_CLASS_CAPTURED;
+  if (stop == GRT_STOP_HORIZON || stop == GRT_STOP_CLOSED_ORBIT) {
+    result = blend(result, XYZA{0.0, 0.0, 0.0, 1.0});
+  } else if (stop == GRT_STOP_CELESTIAL) {
+    double y[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = ws.y[k * n + idx];
+    double th, ph;  // get_as_spherical (point.rs:172-188)
+    double st = 0.0, ct = 0.0;
+    if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
+      th = rem_euclid(y[2], PI);
+      ph = rem_euclid(y[3] + PI, TWO_PI) - PI;
+      sincos(y[2], &st, &ct);
+    } else {
+      double rr;
+      cart_to_sph(y[1], y[2], y[3], &rr, &th, &ph);
+    }
+    double u = (PI + ph) / TWO_PI;
+    double v = th / PI;
+    double vel[4], p[4];
+    stationary_velocity<G>(S, y, ct, vel);
+    momentum<G>(S, rc, y, p);
+    double em = inner<G>(S, y, st, ct, vel, p);
+    double sig0 = signature0<G>();
+    double redshift = (sig0 * rc.obs) / (sig0 * em);
+    result = blend(result, texture_color(S, S.celestial, 1.0 - u, v, redshift, S.celestial_temperature));
+    cls = GRT_CLASS_ESCAPED;
+  }
+  for (int k = nh - 1; k >= 0; --k) result = blend(result, hits[k]);
+  if (opacity >= S.hit_threshold) cls = GRT_CLASS_HIT;
+  if (nrec > GRT_MAX_HITS) {
+    status |= GRT_FLAG_HIT_OVERFLOW;
+    atomicAdd(stats + 3, 1ull);
+  }
+  write_out(out, idx, result, cls, status, stop, steps);
+}
+
 // ------------------------------------------------------------------ launch -------
-hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Outputs& out,
-                        unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
+template <int G>
+static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
+                           unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
+                           hipStream_t stream) {
+  hipLaunchKernelGGL(integrate_kernel<G>, dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws, d_counter,
+                     d_stats);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  unsigned nb = (unsigned)((ws.n + 255) / 256);
+  hipLaunchKernelGGL(shade_kernel<G>, dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
+                        const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
                         int threads, hipStream_t stream) {
-  dim3 grid(blocks), block(threads);
+  if (ws.n == 0) return hipSuccess;
   switch (geometry) {
     case GRT_GEOM_EUCLIDEAN:
-      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_EUCLIDEAN>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
-      break;
+      return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
     case GRT_GEOM_SCHWARZSCHILD:
-      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_SCHWARZSCHILD>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
-      break;
+      return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
     case GRT_GEOM_KERR:
-      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_KERR>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
-      break;
+      return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
     case GRT_GEOM_KERR_BL:
-      hipLaunchKernelGGL(trace_kernel<GRT_GEOM_KERR_BL>, grid, block, 0, stream, d_scene, wl, out, d_counter, d_stats);
-      break;
+      return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 }  // namespace grt

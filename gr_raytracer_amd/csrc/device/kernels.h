@@ -6,9 +6,10 @@
 
 namespace grt {
 
-hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Outputs& out,
-                        unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
-                        int threads, hipStream_t stream);
+// integrate_kernel (persistent, lane refill) then shade_kernel, both on `stream`.
+hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
+                        const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
+                        int blocks, int threads, hipStream_t stream);
 
 // Adaptive supersampling helpers (raytracer.rs:91-159, :320-458).
 struct AdaptiveParams {

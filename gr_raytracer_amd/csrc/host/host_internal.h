@@ -7,7 +7,7 @@
 #include <string>
 #include <vector>
 
-#include "../../../include/grt_api.h"
+#include "grt_api.h"
 
 namespace grt_host {
 

@@ -17,7 +17,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../../../include/grt_api.h"
+#include "grt_api.h"
 #include "host_internal.h"
 
 namespace grt_host {
