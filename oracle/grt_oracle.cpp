@@ -712,6 +712,14 @@ struct StepResult {
   double h_taken, h_next;
   int attempts;
 };
+// Sensitivity probe (tests only): when set, the controller's pow() result is moved by
+// one ulp, to measure how strongly a 1-ulp libm difference propagates on a scene.
+static int g_pow_perturb = 0;
+static inline double controller_pow(double x, double e) {
+  double p = std::pow(x, e);
+  return g_pow_perturb ? std::nextafter(p, INFINITY) : p;
+}
+
 template <int D, class F>
 static Err rkf45(const double* y, double h, double epsilon, const F& f, double* y_new,
                  StepResult* sr) {  // :138-182
@@ -720,7 +728,7 @@ static Err rkf45(const double* y, double h, double epsilon, const F& f, double* 
   for (int it = 0; it < MAX_RETRY_STEP; ++it) {
     double err = rkf45_step<D>(y, h_cur, f, y_new);
     sr->attempts++;
-    double h_prop = err > 0.0 ? BETA * h_cur * std::pow(epsilon / err, 1.0 / CONVERGENCY_ORDER)
+    double h_prop = err > 0.0 ? BETA * h_cur * controller_pow(epsilon / err, 1.0 / CONVERGENCY_ORDER)
                               : h_cur * H_GROWTH_CAP;
     h_prop = rust_clamp(std::fmin(h_prop, h_cur * H_GROWTH_CAP), H_MIN, H_MAX);
     if (err > epsilon) {
@@ -1247,6 +1255,7 @@ using namespace oracle;
 extern "C" {
 
 int oracle_abi_version(void) { return GRT_ABI_VERSION; }
+void oracle_set_pow_perturbation(int on) { g_pow_perturb = on; }
 
 // One ray through Scene::color_of_ray.  use_offset selects get_ray_for_offset.
 int oracle_color_of_ray(const grt_scene_desc* d, int64_t row, int64_t col, int use_offset, double dx,

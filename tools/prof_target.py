@@ -1,0 +1,17 @@
+"""One C2 frame (profiling target): python3 tools/prof_target.py [geometry]"""
+import sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import gr_raytracer_amd as g
+which = sys.argv[1] if len(sys.argv) > 1 else "c2"
+if which == "c2":
+    opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, max_steps=100000)
+    toml = "schwarzschild.toml"
+else:
+    opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-10, 0, -0.5), theta=-3.14159, max_steps=1000000)
+    toml = "kerr-bl.toml"
+hs = g.HostScene(str(ROOT / "tests/golden/scenes" / toml), opts, str(ROOT / "tests/golden"))
+sc = g.Scene(hs.desc_ptr(), keepalive=hs)
+r = sc.render_pixels(0, 0, opts.height, opts.width, aux=False)
+print(r.stats)
