@@ -393,14 +393,22 @@ int grt_scene_destroy(grt_scene* s) {
   return 0;
 }
 
+static int check_rect(const grt_scene* s, uint64_t row0, uint64_t col0, uint64_t rows, uint64_t cols) {
+  if (row0 + rows > (uint64_t)s->desc.camera.rows || col0 + cols > (uint64_t)s->desc.camera.cols)
+    return fail(-EINVAL, "rectangle outside the camera frame");
+  return 0;
+}
+
 int grt_render_pixels_async(grt_scene* s, int device, void* stream, uint32_t row0, uint32_t col0,
                             uint32_t rows, uint32_t cols, float* d_xyza, uint8_t* d_class,
                             uint8_t* d_status, double* d_xyza64, uint32_t* d_steps, uint8_t* d_stop,
                             uint64_t* d_stats) {
   if (!s || !d_xyza || !d_class || !d_status || !d_stats) return fail(-EINVAL, "null argument");
   if (rows == 0 || cols == 0) return 0;
+  int rc = check_rect(s, row0, col0, rows, cols);
+  if (rc) return rc;
   DeviceCopy* dc;
-  int rc = ensure_device(s, device, &dc);
+  rc = ensure_device(s, device, &dc);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(dc->mu);
   HIP_TRY(hipSetDevice(device));
@@ -413,8 +421,10 @@ int grt_render_pixels(grt_scene* s, int device, uint32_t row0, uint32_t col0, ui
                       const grt_offsets* offsets, float* xyza_out, uint8_t* class_out, uint8_t* status_out,
                       const grt_aux_out* aux, grt_stats* stats) {
   if (!s || !xyza_out || !class_out || !status_out) return fail(-EINVAL, "null argument");
+  int rc = check_rect(s, row0, col0, rows, cols);
+  if (rc) return rc;
   DeviceCopy* dc;
-  int rc = ensure_device(s, device, &dc);
+  rc = ensure_device(s, device, &dc);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(dc->mu);
   HIP_TRY(hipSetDevice(device));
@@ -484,8 +494,10 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
   if (!s || !cfg || !xyza_out) return fail(-EINVAL, "null argument");
   if (to_row < from_row || to_col < from_col) return fail(-EINVAL, "empty section");
   if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
+  int rc = check_rect(s, from_row, from_col, to_row - from_row, to_col - from_col);
+  if (rc) return rc;
   DeviceCopy* dc;
-  int rc = ensure_device(s, device, &dc);
+  rc = ensure_device(s, device, &dc);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(dc->mu);
   HIP_TRY(hipSetDevice(device));

@@ -51,6 +51,7 @@ constexpr double INV_ORDER = 1.0 / 5.0;
 constexpr double SMALL_ERR = 1e-5;
 constexpr int MAX_RETRY = 100;
 constexpr double H_MAX = 1.0, H_MIN = 1e-12, H_GROWTH = 4.0;
+constexpr double POW_SATURATED = 1800.0;  // (H_GROWTH / BETA)^5 = 1734.1, plus margin
 
 GDEV double rclamp(double v, double lo, double hi) {  // f64::clamp
   if (v < lo) v = lo;
@@ -889,7 +890,14 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     double yn[8];
     double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
     n_att++;
-    double h_prop = err > 0.0 ? BETA * h_cur * pow(S.epsilon / err, INV_ORDER) : h_cur * H_GROWTH;
+    // h_prop = err > 0 ? BETA*h*(eps/err)^(1/5) : 4h, then min(., 4h).  For eps/err >= 1800,
+    // BETA*1800^(1/5) = 4.0308 > 4, so the min is 4h whatever pow's last ulp: pow is
+    // skipped there (the far-field steps), which leaves every result bit-identical.
+    double h_prop = h_cur * H_GROWTH;
+    if (err > 0.0) {
+      const double ratio = S.epsilon / err;
+      if (ratio < POW_SATURATED) h_prop = BETA * h_cur * pow(ratio, INV_ORDER);
+    }
     h_prop = rclamp(fmin(h_prop, h_cur * H_GROWTH), H_MIN, H_MAX);
     double h_next;
     if (err > S.epsilon) {
