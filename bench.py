@@ -183,7 +183,7 @@ def main() -> None:
                        "frame_wall_s_per_gpu": elapsed / args.steps},
             "roofline": {"bound": "valu-fp64", "achieved": achieved_tflops, "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": traffic, "kernel": "grt::trace_kernel<1> (Schwarzschild)",
+                         "traffic": traffic, "kernel": "grt::integrate_kernel<1> (Schwarzschild; events also span shade_kernel<1>, <0.01%)",
                          "kernel_ms": kernel_ms, "flop_per_launch": flop_per_launch,
                          "flop_model": f"{f_att:g}*attempts + {f_step:g}*accepted (SURVEY 8d)",
                          "hbm_algorithmic_GBps": n * BYTES_PER_PIXEL_OUT / (kernel_ms * 1e-3) / 1e9,

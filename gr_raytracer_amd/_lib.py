@@ -102,6 +102,10 @@ class AuxOut(C.Structure):
     _fields_ = [("xyza64", _pd), ("steps", C.POINTER(C.c_uint32)), ("stop_reason", C.POINTER(C.c_uint8))]
 
 
+class RowShard(C.Structure):
+    _fields_ = [("band_rows", C.c_uint32), ("shard", C.c_uint32), ("n_shards", C.c_uint32)]
+
+
 class GrtError(RuntimeError):
     pass
 
@@ -150,6 +154,11 @@ def lib() -> C.CDLL:
         "grt_render_section": (C.c_int, [vp, C.c_int, u32, u32, u32, u32, C.POINTER(AdaptiveConfig), _pd, _pd,
                                          C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(Stats)]),
         "grt_set_launch_config": (C.c_int, [C.c_int, C.c_int]),
+        "grt_shard_row_count": (u32, [u32, C.POINTER(RowShard)]),
+        "grt_shard_frame_row": (u32, [u32, C.POINTER(RowShard)]),
+        "grt_render_shard": (C.c_int, [vp, C.c_int, C.POINTER(RowShard), C.POINTER(C.c_float), C.POINTER(C.c_uint8),
+                                       C.POINTER(C.c_uint8), C.POINTER(AuxOut), C.POINTER(Stats)]),
+        "grt_render_shard_async": (C.c_int, [vp, C.c_int, vp, C.POINTER(RowShard), vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -166,6 +175,7 @@ EXPORTED_SYMBOLS = [
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
     "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_xyz_to_srgb8", "grt_scene_create", "grt_scene_destroy",
     "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config",
+    "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
 ]
 
 

@@ -399,6 +399,45 @@ static int check_rect(const grt_scene* s, uint64_t row0, uint64_t col0, uint64_t
   return 0;
 }
 
+// Trace `wl` (n output slots) into device scratch, wait, copy to the host arrays.
+static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, uint64_t n, float* xyza_out,
+                       uint8_t* class_out, uint8_t* status_out, const grt_aux_out* aux, grt_stats* stats) {
+  int rc;
+  DeviceCopy* dc = dc_;
+  DevBuf b_xyza, b_cls, b_status, b_x64, b_steps, b_stop;
+  if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n))) return rc;
+  bool want64 = aux && aux->xyza64, want_steps = aux && aux->steps, want_stop = aux && aux->stop_reason;
+  if (want64 && (rc = b_x64.alloc(n * 32))) return rc;
+  if (want_steps && (rc = b_steps.alloc(n * 4))) return rc;
+  if (want_stop && (rc = b_stop.alloc(n))) return rc;
+  grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p,
+                 (uint32_t*)b_steps.p, (uint8_t*)b_stop.p};
+  hipStream_t st = nullptr;
+  HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(dc->ev0, st));
+  if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
+  HIP_TRY(hipEventRecord(dc->ev1, st));
+  HIP_TRY(hipEventSynchronize(dc->ev1));
+  HIP_TRY(hipMemcpy(xyza_out, b_xyza.p, n * 16, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
+  if (want64) HIP_TRY(hipMemcpy(aux->xyza64, b_x64.p, n * 32, hipMemcpyDeviceToHost));
+  if (want_steps) HIP_TRY(hipMemcpy(aux->steps, b_steps.p, n * 4, hipMemcpyDeviceToHost));
+  if (want_stop) HIP_TRY(hipMemcpy(aux->stop_reason, b_stop.p, n, hipMemcpyDeviceToHost));
+  if (stats) {
+    unsigned long long h[4];
+    HIP_TRY(hipMemcpy(h, dc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, dc->ev0, dc->ev1));
+    stats->accepted_steps = h[0];
+    stats->attempts = h[1];
+    stats->rays = h[2];
+    stats->hit_overflows = h[3];
+    stats->kernel_ms = ms;
+  }
+  return 0;
+}
+
 int grt_render_pixels_async(grt_scene* s, int device, void* stream, uint32_t row0, uint32_t col0,
                             uint32_t rows, uint32_t cols, float* d_xyza, uint8_t* d_class,
                             uint8_t* d_status, double* d_xyza64, uint32_t* d_steps, uint8_t* d_stop,
@@ -454,38 +493,7 @@ int grt_render_pixels(grt_scene* s, int device, uint32_t row0, uint32_t col0, ui
   } else {
     wl = rect_worklist(row0, col0, rows, cols);
   }
-  DevBuf b_xyza, b_cls, b_status, b_x64, b_steps, b_stop;
-  if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n))) return rc;
-  bool want64 = aux && aux->xyza64, want_steps = aux && aux->steps, want_stop = aux && aux->stop_reason;
-  if (want64 && (rc = b_x64.alloc(n * 32))) return rc;
-  if (want_steps && (rc = b_steps.alloc(n * 4))) return rc;
-  if (want_stop && (rc = b_stop.alloc(n))) return rc;
-  grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p,
-                 (uint32_t*)b_steps.p, (uint8_t*)b_stop.p};
-  hipStream_t st = nullptr;
-  HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
-  HIP_TRY(hipEventRecord(dc->ev0, st));
-  if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
-  HIP_TRY(hipEventRecord(dc->ev1, st));
-  HIP_TRY(hipEventSynchronize(dc->ev1));
-  HIP_TRY(hipMemcpy(xyza_out, b_xyza.p, n * 16, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
-  if (want64) HIP_TRY(hipMemcpy(aux->xyza64, b_x64.p, n * 32, hipMemcpyDeviceToHost));
-  if (want_steps) HIP_TRY(hipMemcpy(aux->steps, b_steps.p, n * 4, hipMemcpyDeviceToHost));
-  if (want_stop) HIP_TRY(hipMemcpy(aux->stop_reason, b_stop.p, n, hipMemcpyDeviceToHost));
-  if (stats) {
-    unsigned long long h[4];
-    HIP_TRY(hipMemcpy(h, dc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, dc->ev0, dc->ev1));
-    stats->accepted_steps = h[0];
-    stats->attempts = h[1];
-    stats->rays = h[2];
-    stats->hit_overflows = h[3];
-    stats->kernel_ms = ms;
-  }
-  return 0;
+  return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
 }
 
 int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
@@ -605,6 +613,72 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
     stats->kernel_ms = ms;
   }
   return 0;
+}
+
+
+// ------------------------------------------------------------- row-band shards ----
+static int check_shard(const grt_row_shard* sh) {
+  if (!sh) return fail(-EINVAL, "null shard");
+  if (sh->n_shards == 0 || sh->shard >= sh->n_shards) return fail(-EINVAL, "shard index out of range");
+  if (sh->band_rows == 0) return fail(-EINVAL, "band_rows must be >= 1");
+  return 0;
+}
+
+uint32_t grt_shard_row_count(uint32_t frame_rows, const grt_row_shard* sh) {
+  if (!sh || sh->n_shards == 0 || sh->band_rows == 0 || sh->shard >= sh->n_shards) return 0;
+  if (sh->n_shards == 1) return frame_rows;
+  uint64_t bands = ((uint64_t)frame_rows + sh->band_rows - 1) / sh->band_rows;
+  uint64_t mine = bands > sh->shard ? (bands - sh->shard + sh->n_shards - 1) / sh->n_shards : 0;
+  if (mine == 0) return 0;
+  uint64_t last_band = sh->shard + (mine - 1) * sh->n_shards;
+  uint64_t last_rows = std::min<uint64_t>(sh->band_rows, frame_rows - last_band * sh->band_rows);
+  return (uint32_t)((mine - 1) * sh->band_rows + last_rows);
+}
+
+uint32_t grt_shard_frame_row(uint32_t local_row, const grt_row_shard* sh) {
+  if (!sh) return local_row;
+  return grt::shard_frame_row(sh->band_rows, sh->shard, sh->n_shards, local_row);
+}
+
+static grt::WorkList shard_worklist(const grt_scene* s, const grt_row_shard* sh) {
+  uint32_t rows = grt_shard_row_count((uint32_t)s->desc.camera.rows, sh);
+  grt::WorkList wl = rect_worklist(0, 0, rows, (uint32_t)s->desc.camera.cols);
+  wl.band_rows = sh->band_rows;
+  wl.shard = sh->shard;
+  wl.n_shards = sh->n_shards;
+  return wl;
+}
+
+int grt_render_shard(grt_scene* s, int device, const grt_row_shard* sh, float* xyza_out, uint8_t* class_out,
+                     uint8_t* status_out, const grt_aux_out* aux, grt_stats* stats) {
+  if (!s || !xyza_out || !class_out || !status_out) return fail(-EINVAL, "null argument");
+  int rc = check_shard(sh);
+  if (rc) return rc;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  grt::WorkList wl = shard_worklist(s, sh);
+  uint64_t n = (uint64_t)wl.rows * wl.cols;
+  if (n == 0) return 0;
+  DeviceCopy* dc;
+  if ((rc = ensure_device(s, device, &dc))) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
+}
+
+int grt_render_shard_async(grt_scene* s, int device, void* stream, const grt_row_shard* sh, float* d_xyza,
+                           uint8_t* d_class, uint8_t* d_status, double* d_xyza64, uint32_t* d_steps,
+                           uint8_t* d_stop, uint64_t* d_stats) {
+  if (!s || !d_xyza || !d_class || !d_status || !d_stats) return fail(-EINVAL, "null argument");
+  int rc = check_shard(sh);
+  if (rc) return rc;
+  grt::WorkList wl = shard_worklist(s, sh);
+  if ((uint64_t)wl.rows * wl.cols == 0) return 0;
+  DeviceCopy* dc;
+  if ((rc = ensure_device(s, device, &dc))) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  grt::Outputs o{d_xyza, d_class, d_status, d_xyza64, d_steps, d_stop};
+  return enqueue_trace(s, *dc, wl, o, (unsigned long long*)d_stats, (hipStream_t)stream);
 }
 
 }  // extern "C"

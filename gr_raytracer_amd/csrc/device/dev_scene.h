@@ -70,9 +70,10 @@ struct DevScene {
 
 // Work description for one launch.
 struct WorkList {
-  uint32_t row0, col0, rows, cols;
+  uint32_t row0, col0, rows, cols;  // rows = local rows (this shard's rows when sharded)
   uint32_t tiles_x;       // ceil(cols / 8)
-  uint32_t _pad;
+  uint32_t band_rows;     // row-band sharding (grt_row_shard); n_shards <= 1: no sharding
+  uint32_t shard, n_shards;
   uint64_t n_items;       // padded tile items, or offset count
   const uint32_t* pixel_index;  // offsets mode (NULL = rectangle mode)
   const double* dx;
@@ -96,6 +97,16 @@ struct Workspace {
   double* rec_p;      // [4][MAX][n] momentum lerped to the hit (objects.rs:27-44)
   double* rec_pt;     // [3][MAX][n] hit point (sphere-local for spheres)
 };
+
+// Local row -> frame row under cyclic row-band sharding: band k of shard s is frame
+// band k * n_shards + s (grt_api.h, grt_row_shard).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t shard_frame_row(uint32_t band_rows, uint32_t shard, uint32_t n_shards, uint32_t local) {
+  if (n_shards <= 1) return local;
+  return ((local / band_rows) * n_shards + shard) * band_rows + local % band_rows;
+}
 
 #ifndef GRT_INTEGRATE_WAVES
 #define GRT_INTEGRATE_WAVES 2  // min waves per SIMD requested for the integrate kernel

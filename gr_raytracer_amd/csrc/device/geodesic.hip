@@ -851,7 +851,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
             uint32_t tr = (uint32_t)(tile / wl.tiles_x), tc = (uint32_t)(tile % wl.tiles_x);
             uint32_t r = tr * 8 + (w >> 3), cc = tc * 8 + (w & 7);
             valid = (r < wl.rows) && (cc < wl.cols);
-            row = (double)(wl.row0 + r);
+            row = (double)(wl.row0 + shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, r));
             col = (double)(wl.col0 + cc);
             idx = (uint64_t)r * wl.cols + cc;
           }

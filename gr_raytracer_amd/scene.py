@@ -185,6 +185,24 @@ class Scene:
         res.stats = _stats_dict(st)
         return res
 
+    def render_shard(self, band_rows: int, shard: int, n_shards: int, device: int = 0,
+                     aux: bool = True) -> RenderResult:
+        """The local rows of one cyclic row-band shard (grt_render_shard), full width."""
+        sh = L.RowShard(band_rows, shard, n_shards)
+        n = int(L.lib().grt_shard_row_count(self.rows, C.byref(sh))) * self.cols
+        xyza, cls, status = np.zeros((n, 4), np.float32), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+        res = RenderResult(xyza, cls, status)
+        a = None
+        if aux:
+            res.xyza64, res.steps, res.stop_reason = np.zeros((n, 4)), np.zeros(n, np.uint32), np.zeros(n, np.uint8)
+            a = L.AuxOut(L.dptr(res.xyza64), L.ptr(res.steps, C.c_uint32), L.ptr(res.stop_reason, C.c_uint8))
+        st = L.Stats()
+        L.check(L.lib().grt_render_shard(self._s, device, C.byref(sh), L.ptr(xyza, C.c_float), L.ptr(cls, C.c_uint8),
+                                         L.ptr(status, C.c_uint8), C.byref(a) if a is not None else None,
+                                         C.byref(st)), "grt_render_shard")
+        res.stats = _stats_dict(st)
+        return res
+
     def render_section(self, from_row: int = 0, from_col: int = 0, to_row: Optional[int] = None,
                        to_col: Optional[int] = None, adaptive: Optional[L.AdaptiveConfig] = None,
                        sampling_mask_xyza=None, device: int = 0):

@@ -304,6 +304,34 @@ int grt_render_section(grt_scene* scene, int device, uint32_t from_row, uint32_t
                        const double* sampling_mask_xyza, double* xyza_out,
                        uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats);
 
+/* Row-band sharding of one frame across GPUs (multi-GPU render).
+ * The frame's rows are cut into bands of `band_rows` rows (the last may be short);
+ * shard s of n owns the bands b with b % n == s.  Its output is the full-width rows of
+ * those bands, packed in increasing frame order ("local rows").  Cyclic bands balance
+ * the cost, which is concentrated around the shadow and the disc.  The reference has
+ * one process rendering everything (raytracer.rs:195-244); the per-pixel results of a
+ * shard are identical to rendering the same rows through grt_render_pixels. */
+typedef struct grt_row_shard {
+  uint32_t band_rows; /* >= 1; a multiple of 8 keeps the 8x8 pixel tiles inside a band */
+  uint32_t shard;     /* < n_shards */
+  uint32_t n_shards;  /* >= 1 */
+} grt_row_shard;
+
+/* Number of local rows of shard `sh` in a frame of `frame_rows` rows. */
+uint32_t grt_shard_row_count(uint32_t frame_rows, const grt_row_shard* sh);
+/* Frame row of local row `local_row` of shard `sh`. */
+uint32_t grt_shard_frame_row(uint32_t local_row, const grt_row_shard* sh);
+
+/* Trace all local rows of a shard (full frame width) at 1 spp: host outputs,
+ * local-row-major, like grt_render_pixels. */
+int grt_render_shard(grt_scene* scene, int device, const grt_row_shard* sh, float* xyza_out,
+                     uint8_t* class_out, uint8_t* status_out, const grt_aux_out* aux,
+                     grt_stats* stats);
+/* Same with device outputs on `stream`, like grt_render_pixels_async. */
+int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt_row_shard* sh,
+                           float* d_xyza, uint8_t* d_class, uint8_t* d_status, double* d_xyza64,
+                           uint32_t* d_steps, uint8_t* d_stop, uint64_t* d_stats);
+
 /* Kernel launch geometry knobs (persistent grid). 0 = library default. */
 int grt_set_launch_config(int blocks_per_cu, int threads_per_block);
 

@@ -1,0 +1,96 @@
+"""Multi-rank frame assembly on CPU (gloo, world_size 2 and 3).
+
+Each rank renders its cyclic row-band shard (here with the oracle as a stand-in for
+the GPU trace, since this container has no GPU), packs 18-byte pixel records and
+gathers them to rank 0 with gr_raytracer_amd.distributed.gather_frame; rank 0's frame
+must equal a single-process render bit for bit.  The shard row arithmetic is checked
+against the C ABI's grt_shard_row_count / grt_shard_frame_row (host-only calls).
+"""
+import ctypes as C
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, c2_opts, host_scene
+
+FRAME_ROWS, FRAME_COLS = 40, 36
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, band_rows, out_dir):
+    import sys
+
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import gr_raytracer_amd as g
+    import pyoracle as O
+    from gr_raytracer_amd.distributed import gather_frame, pack_records, shard_frame_rows, unpack_records
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hs = host_scene(g, "schwarzschild.toml", c2_opts(g, width=FRAME_COLS, height=FRAME_ROWS))
+        rows = shard_frame_rows(FRAME_ROWS, band_rows, rank, world)
+        r = O.render_pixels(hs.desc, 0, 0, FRAME_ROWS, FRAME_COLS, threads=2, row_list=rows)
+        xyza = torch.from_numpy(r["xyza"].astype(np.float32))
+        rec = pack_records(xyza, torch.from_numpy(r["ray_class"]), torch.from_numpy(r["status"]))
+        frame = gather_frame(rec, FRAME_ROWS, FRAME_COLS, band_rows, rank, world)
+        if rank == 0:
+            fx, fc, fs = unpack_records(frame)
+            np.savez(os.path.join(out_dir, "frame.npz"), xyza=fx.numpy(), cls=fc.numpy(), status=fs.numpy())
+        else:
+            assert frame is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,band_rows", [(2, 8), (3, 16)])
+def test_gloo_sharded_frame_equals_single_process(oracle, grt, world, band_rows):
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), band_rows, d), nprocs=world, join=True)
+        got = np.load(os.path.join(d, "frame.npz"))
+        hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=FRAME_COLS, height=FRAME_ROWS))
+        ref = oracle.render_pixels(hs.desc, 0, 0, FRAME_ROWS, FRAME_COLS, threads=4)
+        assert np.array_equal(got["xyza"], ref["xyza"].astype(np.float32))
+        assert np.array_equal(got["cls"], ref["ray_class"])
+        assert np.array_equal(got["status"], ref["status"])
+
+
+def test_shard_rows_partition_the_frame_and_match_the_c_abi(grt):
+    from gr_raytracer_amd import _lib as L
+    from gr_raytracer_amd.distributed import shard_frame_rows, shard_row_count
+
+    lib = L.lib()
+    for frame_rows in (1, 7, 8, 40, 1500, 4096):
+        for n in (1, 2, 3, 8):
+            for band in (1, 8, 16, 100):
+                seen = []
+                for s in range(n):
+                    sh = L.RowShard(band, s, n)
+                    cnt = shard_row_count(frame_rows, band, s, n)
+                    assert cnt == lib.grt_shard_row_count(frame_rows, C.byref(sh))
+                    rows = shard_frame_rows(frame_rows, band, s, n)
+                    assert len(rows) == cnt
+                    for k in range(0, cnt, max(1, cnt // 7)):
+                        assert rows[k] == lib.grt_shard_frame_row(k, C.byref(sh))
+                    seen.append(rows)
+                allrows = np.sort(np.concatenate(seen))
+                assert np.array_equal(allrows, np.arange(frame_rows)), (frame_rows, n, band)
+    # invalid shards have no rows
+    assert lib.grt_shard_row_count(100, C.byref(L.RowShard(8, 2, 2))) == 0
+    assert lib.grt_shard_row_count(100, C.byref(L.RowShard(0, 0, 2))) == 0

@@ -268,3 +268,21 @@ def test_below_isco_status(grt, oracle, gpu):
     ref, pert = oracle_pair(oracle, d, 0, 0, 48, 48)
     assert (ref["status"] == 3).sum() > 50  # the scene does reach inside the ISCO
     check_parity(got, ref, pert)
+
+
+# ------------------------------------------------------------- multi-GPU shards --
+@pytest.mark.parametrize("n_shards,band_rows", [(2, 8), (3, 16), (8, 16)])
+def test_row_shards_reassemble_the_frame(grt, gpu, n_shards, band_rows):
+    """grt_render_shard (cyclic row bands) is bit-identical to the frame."""
+    from gr_raytracer_amd.distributed import shard_frame_rows
+
+    hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=120, height=100))
+    sc = gpu_scene(grt, hs)
+    full = sc.render_pixels(0, 0, 100, 120)
+    f64 = full.xyza64.reshape(100, 120, 4)
+    steps = full.steps.reshape(100, 120)
+    for s in range(n_shards):
+        part = sc.render_shard(band_rows, s, n_shards)
+        rows = shard_frame_rows(100, band_rows, s, n_shards)
+        assert np.array_equal(part.xyza64.reshape(len(rows), 120, 4), f64[rows])
+        assert np.array_equal(part.steps.reshape(len(rows), 120), steps[rows])
