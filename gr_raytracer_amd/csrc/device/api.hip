@@ -177,6 +177,14 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   ds.step_size = d.step_size;
   ds.epsilon = d.epsilon;
   ds.trapped_radius = 5.0 * d.radius;
+  // Far-field filter bounds.  The margins (1e-9 relative) are ~1e6 x the rounding of
+  // the Cartesian conversion and of the chord arithmetic, so every window the filter
+  // skips would have been a miss in the reference too ("Exact skips").
+  ds.far_ok = (d.geometry == GRT_GEOM_SCHWARZSCHILD || d.geometry == GRT_GEOM_KERR_BL) ? 1 : 0;
+  ds.far_a = d.geometry == GRT_GEOM_KERR_BL ? std::fabs(d.a) : 0.0;
+  ds.cel_lo2 = ds.max_radius_sq * (1.0 - 1e-9);
+  ds.cel_hi2 = ds.max_radius_sq * (1.0 + 1e-9);
+  if (!std::isfinite(ds.far_a) || !std::isfinite(ds.max_radius_sq)) ds.far_ok = 0;
   const grt_camera_desc& c = d.camera;
   for (int k = 0; k < 4; ++k) {
     ds.cam.pos[k] = c.position[k];
@@ -214,6 +222,13 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     q.rout = o.outer_radius;
     q.rin2 = o.inner_radius * o.inner_radius;
     q.rout2 = o.outer_radius * o.outer_radius;
+    {
+      double cn = std::sqrt(o.center[0] * o.center[0] + o.center[1] * o.center[1] + o.center[2] * o.center[2]);
+      double R = std::fabs(o.radius);
+      q.shell_lo = (cn - R) * (1.0 - 1e-9) - 1e-9;
+      q.shell_hi = (cn + R) * (1.0 + 1e-9) + 1e-9;
+      if (!std::isfinite(q.shell_lo) || !std::isfinite(q.shell_hi)) ds.far_ok = 0;
+    }
     q.temp_constant = o.temp_constant;
     q.r_isco = o.r_isco;
     q.lut_n = o.lut_n;

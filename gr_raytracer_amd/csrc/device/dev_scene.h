@@ -26,6 +26,9 @@ struct DevObject {
   double temperature; // sphere constant temperature
   double rin, rout, rin2, rout2;  // disc annulus
   double temp_constant, r_isco;
+  // far-field filter (integrate_kernel): a sphere cannot be hit from a window whose two
+  // ends have Cartesian radius outside [shell_lo, shell_hi] (margins 1e-9, see api.hip)
+  double shell_lo, shell_hi;
   const double* lut_r;
   const double* lut_t;
   uint32_t lut_n;
@@ -55,6 +58,11 @@ struct DevScene {
   uint64_t max_steps;
   double max_radius_sq, step_size, epsilon;
   double trapped_radius;  // TRAPPED_ORBIT_RADIUS_FACTOR * radius
+  // far-field filter: Cartesian radius of a state is within [r, r + far_a]; the
+  // celestial test |x|^2 > max_radius^2 is decided from r outside [cel_lo2, cel_hi2]
+  int32_t far_ok;         // geometry has a curvilinear chart (Schwarzschild / KerrBL)
+  int32_t _pad2;
+  double far_a, cel_lo2, cel_hi2;
   DevCamera cam;
   DevTexture celestial;
   double celestial_temperature;

@@ -761,7 +761,7 @@ GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayCons
 
 // integrator.rs:203-268
 template <int G>
-GDEV int should_stop(const DevScene& S, const double* y, const double* c, uint64_t i) {
+GDEV int should_stop(const DevScene& S, const double* y, double* c, bool& c_valid, uint64_t i) {
   if (!(isfinite(y[0]) && isfinite(y[1]) && isfinite(y[2]) && isfinite(y[3]))) return GRT_STOP_NAN;
   bool last = (i == S.max_steps - 1);
   if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
@@ -774,9 +774,63 @@ GDEV int should_stop(const DevScene& S, const double* y, const double* c, uint64
     if (S.has_horizon && r <= S.horizon_r) return GRT_STOP_HORIZON;
     if (last && r < S.trapped_radius) return GRT_STOP_CLOSED_ORBIT;
   }
-  if (c[0] * c[0] + c[1] * c[1] + c[2] * c[2] > S.max_radius_sq) return GRT_STOP_CELESTIAL;
+  // celestial test |x_cart|^2 > max_radius^2 (integrator.rs:203-268).  |x_cart| lies in
+  // [|r|, |r| + far_a] in the curvilinear charts, so away from the celestial shell the
+  // answer follows from r and the conversion is skipped.
+  bool escaped = false, decided = false;
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
+    if (!c_valid && S.far_ok) {
+      double ar = fabs(y[1]), hi = ar + S.far_a;
+      if (hi * hi < S.cel_lo2) decided = true;
+      else if (ar * ar > S.cel_hi2) decided = escaped = true;
+    }
+  }
+  if (!decided) {
+    if (!c_valid) {
+      to_cart<G>(S, y, c);
+      c_valid = true;
+    }
+    escaped = c[0] * c[0] + c[1] * c[1] + c[2] * c[2] > S.max_radius_sq;
+  }
+  if (escaped) return GRT_STOP_CELESTIAL;
   if (!(isfinite(y[4]) && isfinite(y[5]) && isfinite(y[6]) && isfinite(y[7]))) return GRT_STOP_NAN;
   return GRT_STOP_NONE;
+}
+
+// Exact far-field window filter (curvilinear charts).  True when neither end of the
+// window (ya -> yb) can produce a hit in the reference's chord tests, decided from r and
+// theta alone, so the Cartesian conversion and the chord arithmetic can be skipped:
+//  * Disc (disc.rs:41-88): z = r cos(theta) keeps one strict sign, with |z| >= 1e-9 r at
+//    both ends and r_a / r_b within [1e-3, 1e3], so t = -z_a / (z_b - z_a) is outside
+//    [0, 1] by a factor ~1e-12, far above rounding (theta within 1e-9 of a zero of cos,
+//    or outside (-pi/2, 3pi/2), is always converted).
+//  * Sphere (sphere.rs:37-128): a hit needs |x - c|^2 - R^2 to change sign over the
+//    window; |x| in [r, r + far_a] outside the host's shell [shell_lo, shell_hi]
+//    (1e-9 margins) keeps both ends strictly outside.
+template <int G>
+GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
+  if constexpr (G != GRT_GEOM_SCHWARZSCHILD && G != GRT_GEOM_KERR_BL) {
+    return false;
+  } else {
+    if (!S.far_ok) return false;
+    const double ra = ya[1], rb = yb[1], ta = ya[2], tb = yb[2];
+    constexpr double N_LO = -1.5707963257948966, N_HI = 1.5707963257948966;  // (-pi/2, pi/2) -/+ 1e-9
+    constexpr double S_LO = 1.5707963277948966, S_HI = 4.7123889793846899;   // (pi/2, 3pi/2) +/- 1e-9
+    for (uint32_t k = 0; k < S.n_objects; ++k) {
+      const DevObject& o = S.obj[k];
+      if (o.kind == GRT_OBJ_DISC) {
+        bool north = ta > N_LO && ta < N_HI && tb > N_LO && tb < N_HI;
+        bool south = ta > S_LO && ta < S_HI && tb > S_LO && tb < S_HI;
+        if (!(north || south)) return false;
+        if (!(ra >= 1e-3 * rb && rb >= 1e-3 * ra && ra > 0.0)) return false;
+      } else {
+        bool out_a = ra > o.shell_hi || fabs(ra) + S.far_a < o.shell_lo;
+        bool out_b = rb > o.shell_hi || fabs(rb) + S.far_a < o.shell_lo;
+        if (!(out_a && out_b)) return false;
+      }
+    }
+    return true;
+  }
 }
 
 // End of a ray: its final state goes to the workspace for the shade kernel.
@@ -810,7 +864,8 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   bool active = false, done = false;
   uint64_t idx = 0;      // output slot of the current ray
   double y[8];           // state
-  double c[3];           // Cartesian position of the last accepted step
+  double c[3];           // Cartesian position of the last accepted step (when c_valid)
+  bool c_valid = false;
   double h = 0.0, h_cur = 0.0;
   uint64_t i = 0;        // accepted step index
   int retries = 0;
@@ -861,7 +916,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
             ws.rc[1 * n + idx] = rc.e;
             ws.rc[2 * n + idx] = rc.lz;
             ws.rc[3 * n + idx] = rc.q;
-            to_cart<G>(S, y, c);
+            c_valid = false;
             h = S.step_size;
             h_cur = rclamp(h, H_MIN, H_MAX);
             i = 0;
@@ -919,46 +974,52 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     h = h_next;
     i++;
     n_acc++;
-    double cn[3];
-    to_cart<G>(S, yn, cn);
-    // window (y -> yn) against every object; record each new nearest candidate
-    double shortest = 1.7976931348623157e308;
-    for (uint32_t k = 0; k < S.n_objects; ++k) {
-      const DevObject& o = S.obj[k];
-      double t, pt[3];
-      bool hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
-      if (!hit) continue;
-      double wx = pt[0], wy = pt[1], wz = pt[2];
-      if (o.kind != GRT_OBJ_DISC) {
-        wx = pt[0] + o.cx;
-        wy = pt[1] + o.cy;
-        wz = pt[2] + o.cz;
-      }
-      double dx = wx - c[0], dy = wy - c[1], dz = wz - c[2];
-      double distance = sqrt(dx * dx + dy * dy + dz * dz);
-      if (!(distance < shortest)) continue;
-      shortest = distance;
-      if (nrec < GRT_MAX_HITS) {
-        double pa[4], pb[4];
-        momentum<G>(S, rc, y, pa);
-        momentum<G>(S, rc, yn, pb);
-        double sw = 1.0 - t;
-        const uint64_t slot = (uint64_t)nrec * n + idx;
-        ws.rec_win[slot] = (uint32_t)i;
-        ws.rec_obj[slot] = (uint8_t)k;
+    if (!window_far<G>(S, y, yn)) {
+      if (!c_valid) to_cart<G>(S, y, c);
+      double cn[3];
+      to_cart<G>(S, yn, cn);
+      // window (y -> yn) against every object; record each new nearest candidate
+      double shortest = 1.7976931348623157e308;
+      for (uint32_t k = 0; k < S.n_objects; ++k) {
+        const DevObject& o = S.obj[k];
+        double t, pt[3];
+        bool hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
+        if (!hit) continue;
+        double wx = pt[0], wy = pt[1], wz = pt[2];
+        if (o.kind != GRT_OBJ_DISC) {
+          wx = pt[0] + o.cx;
+          wy = pt[1] + o.cy;
+          wz = pt[2] + o.cz;
+        }
+        double dx = wx - c[0], dy = wy - c[1], dz = wz - c[2];
+        double distance = sqrt(dx * dx + dy * dy + dz * dz);
+        if (!(distance < shortest)) continue;
+        shortest = distance;
+        if (nrec < GRT_MAX_HITS) {
+          double pa[4], pb[4];
+          momentum<G>(S, rc, y, pa);
+          momentum<G>(S, rc, yn, pb);
+          double sw = 1.0 - t;
+          const uint64_t slot = (uint64_t)nrec * n + idx;
+          ws.rec_win[slot] = (uint32_t)i;
+          ws.rec_obj[slot] = (uint8_t)k;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
+          for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
+          for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
+        }
+        nrec++;
       }
-      nrec++;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) c[k] = cn[k];
+      c_valid = true;
+    } else {
+      c_valid = false;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) y[k] = yn[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) c[k] = cn[k];
 
-    int stop = should_stop<G>(S, y, c, i);
+    int stop = should_stop<G>(S, y, c, c_valid, i);
     if (stop != GRT_STOP_NONE || i == S.max_steps - 1) {
       store_ray(ws, idx, y, stop, GRT_OK, nrec, (uint32_t)i);
       active = false;

@@ -254,6 +254,26 @@ struct Ray {  // rendering/ray.rs:16-23
   FourVector momentum;
 };
 
+// Sensitivity probes (tests only).  Bit mask: 1 = controller pow() one ulp up,
+// 2 = one ulp down, 4 = the RHS's sin() one ulp up and cos() one ulp down.  Used to
+// measure how strongly a last-ulp libm difference propagates on a scene; a pixel that
+// moves under any probe is "libm-sensitive" (tests/test_gpu_parity.py).
+static int g_libm_probe = 0;
+static inline double controller_pow(double x, double e) {
+  double p = std::pow(x, e);
+  if (g_libm_probe & 1) return std::nextafter(p, INFINITY);
+  if (g_libm_probe & 2) return std::nextafter(p, -INFINITY);
+  return p;
+}
+static inline double rhs_sin(double x) {
+  double v = std::sin(x);
+  return (g_libm_probe & 4) ? std::nextafter(v, INFINITY) : v;
+}
+static inline double rhs_cos(double x) {
+  double v = std::cos(x);
+  return (g_libm_probe & 4) ? std::nextafter(v, -INFINITY) : v;
+}
+
 struct GeodesicSolver {  // geometry.rs:15-32
   virtual ~GeodesicSolver() {}
   virtual void apply(const double* y, double* out) const = 0;
@@ -322,10 +342,10 @@ struct SchwarzschildSolver : GeodesicSolver {
     double aprime_over_a = a_prime / a;
     double a_t = -(aprime_over_a)*v_t * v_r;
     double a_r = -0.5 * a * a_prime * v_t * v_t + 0.5 * (aprime_over_a)*v_r * v_r +
-                 a * r * (v_theta * v_theta + v_phi * v_phi * std::sin(theta) * std::sin(theta));
-    double a_theta = -(2.0 / r) * v_r * v_theta + std::sin(theta) * std::cos(theta) * v_phi * v_phi;
+                 a * r * (v_theta * v_theta + v_phi * v_phi * rhs_sin(theta) * rhs_sin(theta));
+    double a_theta = -(2.0 / r) * v_r * v_theta + rhs_sin(theta) * rhs_cos(theta) * v_phi * v_phi;
     double a_phi =
-        -(2.0 / r) * v_phi * v_r - 2.0 * std::cos(theta) / std::sin(theta) * v_theta * v_phi;
+        -(2.0 / r) * v_phi * v_r - 2.0 * rhs_cos(theta) / rhs_sin(theta) * v_theta * v_phi;
     o[0] = v_t; o[1] = v_r; o[2] = v_theta; o[3] = v_phi;
     o[4] = a_t; o[5] = a_r; o[6] = a_theta; o[7] = a_phi;
   }
@@ -549,7 +569,7 @@ struct KerrBLSolver : GeodesicSolver {
     double r = y[1], theta = y[2], v_r = y[4], v_theta = y[5];
     double del = bl_delta(r, radius, a);
     double p_r = (r * r + a * a) * e - a * l_z;
-    double sin_t = std::sin(theta);
+    double sin_t = rhs_sin(theta);
     double sin2 = sin_t * sin_t;
     double dt = (r * r + a * a) / del * p_r + a * (l_z - a * e * sin2);
     double dphi = a / del * p_r + l_z / sin2 - a * e;
@@ -559,7 +579,7 @@ struct KerrBLSolver : GeodesicSolver {
     double carter = le * le + q;
     double dv_r = (4.0 * r * e * p_r2 - (2.0 * r - radius) * carter) / 2.0;
     // potential_theta_derivative :114-118
-    double cos_t = std::cos(theta), sin_t2 = std::sin(theta);
+    double cos_t = rhs_cos(theta), sin_t2 = rhs_sin(theta);
     double dv_theta = (-2.0 * a * a * e * e * cos_t * sin_t2 +
                        2.0 * l_z * l_z * cos_t / (sin_t2 * (sin_t2 * sin_t2))) /
                       2.0;
@@ -712,14 +732,6 @@ struct StepResult {
   double h_taken, h_next;
   int attempts;
 };
-// Sensitivity probe (tests only): when set, the controller's pow() result is moved by
-// one ulp, to measure how strongly a 1-ulp libm difference propagates on a scene.
-static int g_pow_perturb = 0;
-static inline double controller_pow(double x, double e) {
-  double p = std::pow(x, e);
-  return g_pow_perturb ? std::nextafter(p, INFINITY) : p;
-}
-
 template <int D, class F>
 static Err rkf45(const double* y, double h, double epsilon, const F& f, double* y_new,
                  StepResult* sr) {  // :138-182
@@ -1255,7 +1267,7 @@ using namespace oracle;
 extern "C" {
 
 int oracle_abi_version(void) { return GRT_ABI_VERSION; }
-void oracle_set_pow_perturbation(int on) { g_pow_perturb = on; }
+void oracle_set_libm_perturbation(int mode) { g_libm_probe = mode; }
 
 // One ray through Scene::color_of_ray.  use_offset selects get_ray_for_offset.
 int oracle_color_of_ray(const grt_scene_desc* d, int64_t row, int64_t col, int use_offset, double dx,

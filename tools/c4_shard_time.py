@@ -1,0 +1,25 @@
+"""C4 (4096^2 kerr.toml, Kerr-Schild) on one GPU: time the row-band shards an 8-GPU
+node would give each rank (band 16), to size the multi-GPU C4 run."""
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import gr_raytracer_amd as g  # noqa: E402
+
+opts = g.GlobalOpts(width=4096, height=4096, camera_position=(-10.0, 0.0, -0.5), theta=1.52, psi=-1.57,
+                    max_steps=1000000)
+hs = g.HostScene(str(ROOT / "tests/golden/scenes/kerr.toml"), opts, str(ROOT / "tests/golden"))
+sc = g.Scene(hs.desc_ptr(), keepalive=hs)
+n_shards = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+shards = [int(x) for x in sys.argv[2:]] or [0, n_shards // 2]
+for s in shards:
+    t = time.time()
+    r = sc.render_shard(16, s, n_shards, aux=False)
+    st = r.stats
+    print(json.dumps({"shard": s, "n_shards": n_shards, "rays": st["rays"], "wall_s": round(time.time() - t, 3),
+                      "kernel_ms": st["kernel_ms"], "accepted": st["accepted_steps"], "attempts": st["attempts"],
+                      "steps_per_s": st["accepted_steps"] / (st["kernel_ms"] * 1e-3),
+                      "overflows": st["hit_overflows"]}), flush=True)
