@@ -137,13 +137,41 @@ static inline double quad_form(const double* v, const Mat4& M, const double* w) 
 }
 
 // ------------------------------------------------------ chart conversions ----
+// Sensitivity probes (tests only).  Bit mask: 1 = controller pow() one ulp up,
+// 2 = one ulp down, 4 = the RHS's sin() one ulp up and cos() one ulp down, 8 / 16 =
+// shading angles one ulp up / down (see shade_angle).  Used to
+// measure how strongly a last-ulp libm difference propagates on a scene; a pixel that
+// moves under any probe is "libm-sensitive" (tests/test_gpu_parity.py).
+static int g_libm_probe = 0;
+static inline double controller_pow(double x, double e) {
+  double p = std::pow(x, e);
+  if (g_libm_probe & 1) return std::nextafter(p, INFINITY);
+  if (g_libm_probe & 2) return std::nextafter(p, -INFINITY);
+  return p;
+}
+static inline double rhs_sin(double x) {
+  double v = std::sin(x);
+  return (g_libm_probe & 4) ? std::nextafter(v, INFINITY) : v;
+}
+// probe bits 8 / 16: shading angles (atan2 / acos of hit points and of the final
+// direction, which feed texture coordinates) one ulp up / down
+static inline double shade_angle(double v) {
+  if (g_libm_probe & 8) return std::nextafter(v, INFINITY);
+  if (g_libm_probe & 16) return std::nextafter(v, -INFINITY);
+  return v;
+}
+static inline double rhs_cos(double x) {
+  double v = std::cos(x);
+  return (g_libm_probe & 4) ? std::nextafter(v, -INFINITY) : v;
+}
+
 // spherical_coordinates_helper.rs:5-26
 static Point cartesian_to_spherical(const Point& c) {
   double t = c[0], x = c[1], y = c[2], z = c[3];
   double r = std::sqrt(x * x + y * y + z * z);
   if (r == 0.0) return Point{CS::Spherical, 0.0, {t, 0.0, 0.0, 0.0}};
-  double theta = std::acos(z / r);
-  double phi = std::atan2(y, x);
+  double theta = shade_angle(std::acos(z / r));
+  double phi = shade_angle(std::atan2(y, x));
   return Point{CS::Spherical, 0.0, {t, r, theta, phi}};
 }
 // :28-39
@@ -161,8 +189,8 @@ static Point cartesian_to_boyer_lindquist(double a, const Point& c) {
   double d = rho_sqr - a * a;
   double r_sqr = 0.5 * (rho_sqr - a * a + std::sqrt(d * d + 4.0 * a * a * z * z));
   double r = std::sqrt(r_sqr);
-  double theta = (r == 0.0) ? 0.0 : std::acos(rust_clamp(z / r, -1.0, 1.0));
-  double phi = std::atan2(r * y - a * x, r * x + a * y);
+  double theta = (r == 0.0) ? 0.0 : shade_angle(std::acos(rust_clamp(z / r, -1.0, 1.0)));
+  double phi = shade_angle(std::atan2(r * y - a * x, r * x + a * y));
   return Point{CS::BoyerLindquist, a, {t, r, theta, phi}};
 }
 // point.rs:139-154
@@ -254,25 +282,6 @@ struct Ray {  // rendering/ray.rs:16-23
   FourVector momentum;
 };
 
-// Sensitivity probes (tests only).  Bit mask: 1 = controller pow() one ulp up,
-// 2 = one ulp down, 4 = the RHS's sin() one ulp up and cos() one ulp down.  Used to
-// measure how strongly a last-ulp libm difference propagates on a scene; a pixel that
-// moves under any probe is "libm-sensitive" (tests/test_gpu_parity.py).
-static int g_libm_probe = 0;
-static inline double controller_pow(double x, double e) {
-  double p = std::pow(x, e);
-  if (g_libm_probe & 1) return std::nextafter(p, INFINITY);
-  if (g_libm_probe & 2) return std::nextafter(p, -INFINITY);
-  return p;
-}
-static inline double rhs_sin(double x) {
-  double v = std::sin(x);
-  return (g_libm_probe & 4) ? std::nextafter(v, INFINITY) : v;
-}
-static inline double rhs_cos(double x) {
-  double v = std::cos(x);
-  return (g_libm_probe & 4) ? std::nextafter(v, -INFINITY) : v;
-}
 
 struct GeodesicSolver {  // geometry.rs:15-32
   virtual ~GeodesicSolver() {}
@@ -979,7 +988,7 @@ static bool disc_intersects(const grt_object_desc& o, const Point& ys, const Poi
   double rin = o.inner_radius, rout = o.outer_radius;
   if (rr >= rin * rin && rr <= rout * rout) {
     double vx = ip.x - 0.0, vy = ip.y - 0.0;
-    double phi = std::atan2(vy, vx);
+    double phi = shade_angle(std::atan2(vy, vx));
     double r = (std::sqrt(rr) - rin) / (rout - rin);
     out->u = 0.5 + 0.5 * r * std::cos(phi);
     out->v = 0.5 + 0.5 * r * std::sin(phi);

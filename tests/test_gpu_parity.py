@@ -38,7 +38,7 @@ def gpu_scene(grt, hs):
     return grt.Scene(hs.desc_ptr(), keepalive=hs, adaptive=hs.adaptive)
 
 
-PROBES = (1, 2, 4)  # oracle last-ulp probes: pow +1 ulp, pow -1 ulp, RHS sin/cos +-1 ulp
+PROBES = (1, 2, 4, 8, 16)  # oracle last-ulp probes: pow +-1 ulp, RHS sin/cos, shading angles +-1 ulp
 
 
 def oracle_pair(oracle, desc, *args, **kw):
