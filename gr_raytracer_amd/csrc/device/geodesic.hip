@@ -20,17 +20,26 @@
 // Floating point follows the reference's evaluation order (Rust, no contraction);
 // the library is compiled with -ffp-contract=off.  Per-frame constants that need
 // libm (sin/cos of the camera position, tan(alpha/2), LUTs) are evaluated on the
-// host, so only per-step transcendentals use the device libm (OCML).
+// host.  pow() is glibc's own algorithm restated bit-exactly (glibc_math.h); the
+// remaining per-step transcendentals (sin/cos/atan2/acos) use the device libm (OCML).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "grt_api.h"
 #include "dev_scene.h"
+#include "glibc_math.h"
 #include "kernels.h"
 
 namespace grt {
 
 #define GDEV __device__ __forceinline__
+
+// f64::powf == glibc pow: bit-exact on glibc's fast path, OCML outside it.
+GDEV double rpow(double x, double y) {
+  double r;
+  if (glibc::pow_fast(x, y, &r)) return r;
+  return pow(x, y);
+}
 
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
@@ -512,7 +521,7 @@ GDEV bool killing_coefficients(const DevScene& S, double r, double* u_t, double*
   double r_s = S.radius, a = S.a;
   double m = 0.5 * r_s;
   double sqrt_m = sqrt(m);
-  double omega = sqrt_m / (pow(r, 1.5) + a * sqrt_m);
+  double omega = sqrt_m / (rpow(r, 1.5) + a * sqrt_m);
   double c = S.cos_half_pi, s = S.sin_half_pi;
   double sig = r * r + a * a * (c * c);
   double sin2 = s * s;
@@ -599,7 +608,7 @@ GDEV XYZA texture_color(const DevScene& S, const DevTexture& t, double u, double
   } else {
     c = sample_blackbody(S, temperature * redshift);
   }
-  double f = pow(redshift, t.beaming);  // apply_beaming (color.rs:72-80)
+  double f = rpow(redshift, t.beaming);  // apply_beaming (color.rs:72-80)
   return XYZA{c.x * f, c.y * f, c.z * f, c.a};
 }
 
@@ -951,7 +960,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     double h_prop = h_cur * H_GROWTH;
     if (err > 0.0) {
       const double ratio = S.epsilon / err;
-      if (ratio < POW_SATURATED) h_prop = BETA * h_cur * pow(ratio, INV_ORDER);
+      if (ratio < POW_SATURATED) h_prop = BETA * h_cur * rpow(ratio, INV_ORDER);
     }
     h_prop = rclamp(fmin(h_prop, h_cur * H_GROWTH), H_MIN, H_MAX);
     double h_next;

@@ -1,0 +1,40 @@
+"""The device pow (gr_raytracer_amd/csrc/device/glibc_math.h), compiled for the host,
+returns glibc's pow bits on its whole fast path (CPU only).
+
+f64::powf in the reference is glibc pow; on x86-64 with FMA glibc 2.35 runs
+__pow_fma, whose operation sequence glibc_math.h restates.  The tables come from the
+installed libm (tools/gen_glibc_tables.py); this test re-derives them too, so a libm
+update that changes them is caught here."""
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+DEV = ROOT / "gr_raytracer_amd" / "csrc" / "device"
+MODES = {0: "controller eps/err over 1e-304..1e304, y = 1/5", 1: "controller range", 2: "beaming exponents",
+         3: "x near 1", 4: "random normal x, |y| < 2"}
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("glibc") / "check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", str(DEV),
+                    str(ROOT / "tests" / "native" / "glibc_pow_check.cpp"), "-o", str(exe)], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_device_pow_is_bit_identical_to_glibc(checker, mode):
+    out = subprocess.run([str(checker), str(mode), "400000"], check=True, capture_output=True, text=True).stdout
+    n, fast, bad = map(int, out.strip().splitlines()[-1].split())
+    assert bad == 0, out
+    assert fast >= 0.7 * n, (MODES[mode], fast, n)
+    if mode in (0, 1):
+        assert fast == n  # the controller's inputs are always on the fast path
+
+
+def test_tables_match_the_installed_libm():
+    gen = subprocess.run(["python3", str(ROOT / "tools" / "gen_glibc_tables.py")], check=True, capture_output=True,
+                         text=True).stdout
+    assert gen == (DEV / "glibc_tables.h").read_text()

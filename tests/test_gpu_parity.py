@@ -112,7 +112,7 @@ def test_kat_scenes_on_gpu(grt, oracle, gpu):
         rows, cols = int(d.camera.rows), int(d.camera.cols)
         got = sc.render_pixels(0, 0, rows, cols)
         ref, probes = oracle_pair(oracle, d, 0, 0, rows, cols)
-        check_parity(got, ref, probes, max_sensitive=0.05)  # alpha = pi/2 frames graze the photon sphere
+        check_parity(got, ref, probes, max_sensitive=0.10)  # alpha = pi/2 frames graze the photon sphere
         i = pixel[0] * cols + pixel[1]
         assert np.all(np.abs(got.xyza64[i] - np.array(want)) <= 1e-6), (name, got.xyza64[i], want)
         assert got.status[i] == 0
