@@ -40,6 +40,22 @@ GDEV double rpow(double x, double y) {
   if (glibc::pow_fast(x, y, &r)) return r;
   return pow(x, y);
 }
+// f64::sin / f64::cos of one operand in one reference function: the compiler fuses
+// them into glibc's sincos (glibc_math.h); a lone sin() stays glibc's sin.  Both are
+// bit-exact for |x| < 105414350; OCML beyond (never reached by angles here).
+GDEV void rsincos(double x, double* s, double* c) {
+  if (!glibc::sincos_fast(x, s, c)) sincos(x, s, c);
+}
+GDEV double rsin(double x) {
+  double r;
+  if (glibc::sin_fast(x, &r)) return r;
+  return sin(x);
+}
+GDEV double rcos(double x) {
+  double r;
+  if (glibc::cos_fast(x, &r)) return r;
+  return cos(x);
+}
 
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
@@ -250,7 +266,7 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
     double st, ct;
-    sincos(theta, &st, &ct);
+    rsincos(theta, &st, &ct);
     double a = 1.0 - radius / r;
     double a_prime = radius / (r * r);
     double aprime_over_a = a_prime / a;
@@ -268,7 +284,7 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     double radius = S.radius, a = S.a, e = rc.e, l_z = rc.lz, q = rc.q;
     double r = y[1], theta = y[2];
     double st, ct;
-    sincos(theta, &st, &ct);
+    rsincos(theta, &st, &ct);
     double del = bl_delta(r, radius, a);
     double r2a2 = r * r + a * a;
     double p_r = r2a2 * e - a * l_z;
@@ -387,8 +403,8 @@ template <int G>
 GDEV void to_cart(const DevScene& S, const double* y, double* c) {
   if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
     double st, ct, sp, cp;
-    sincos(y[2], &st, &ct);
-    sincos(y[3], &sp, &cp);
+    rsincos(y[2], &st, &ct);
+    rsincos(y[3], &sp, &cp);
     double r = y[1];
     c[0] = r * st * cp;
     c[1] = r * st * sp;
@@ -396,8 +412,8 @@ GDEV void to_cart(const DevScene& S, const double* y, double* c) {
   } else if constexpr (G == GRT_GEOM_KERR_BL) {
     double a = S.a, r = y[1];
     double st, ct, sp, cp;
-    sincos(y[2], &st, &ct);
-    sincos(y[3], &sp, &cp);
+    rsincos(y[2], &st, &ct);
+    rsincos(y[3], &sp, &cp);
     c[0] = (r * cp - a * sp) * st;
     c[1] = (r * sp + a * cp) * st;
     c[2] = r * ct;
@@ -439,7 +455,7 @@ GDEV void momentum(const DevScene& S, const RayConst& rc, const double* y, doubl
     double a = S.a, e = rc.e, l_z = rc.lz;
     double r = y[1], theta = y[2], v_r = y[4], v_theta = y[5];
     double st, ct;
-    sincos(theta, &st, &ct);
+    rsincos(theta, &st, &ct);
     double del = bl_delta(r, S.radius, a);
     double sig = r * r + a * a * (ct * ct);
     double sin2 = st * st;
@@ -494,7 +510,7 @@ GDEV double signature0() {
 
 // get_stationary_velocity_at (schwarzschild.rs:237-240; kerr.rs:449-455; kerr_bl.rs:362-371)
 template <int G>
-GDEV void stationary_velocity(const DevScene& S, const double* pos, double ct, double* u) {
+GDEV void stationary_velocity(const DevScene& S, const double* pos, double* u) {
   u[1] = 0.0;
   u[2] = 0.0;
   u[3] = 0.0;
@@ -503,6 +519,7 @@ GDEV void stationary_velocity(const DevScene& S, const double* pos, double ct, d
     u[0] = 1.0 / sqrt(a);
   } else if constexpr (G == GRT_GEOM_KERR_BL) {
     double r = pos[1];
+    double ct = rcos(pos[2]);  // kerr_bl.rs:362-371 evaluates sigma alone: a lone cos()
     double sig = r * r + S.a * S.a * (ct * ct);
     u[0] = 1.0 / sqrt(1.0 - S.radius * r / sig);
   } else if constexpr (G == GRT_GEOM_KERR) {
@@ -1067,7 +1084,7 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
     double phi = atan2(wy - 0.0, wx - 0.0);
     double r = (sqrt(rr) - o.rin) / (o.rout - o.rin);
     double sp, cp;
-    sincos(phi, &sp, &cp);
+    rsincos(phi, &sp, &cp);
     u_tex = 0.5 + 0.5 * r * cp;
     v_tex = 0.5 + 0.5 * r * sp;
   } else {  // sphere.rs:92-117 uv from the sphere-local point, world point for physics
@@ -1085,10 +1102,10 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
   x[0] = 0.0;
   if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
     cart_to_sph(wx, wy, wz, &x[1], &x[2], &x[3]);
-    sincos(x[2], &st, &ct);
+    st = rsin(x[2]);  // the only trig of schwarzschild.rs:90-102 (ct unused)
   } else if constexpr (G == GRT_GEOM_KERR_BL) {
     cart_to_bl(S.a, wx, wy, wz, &x[1], &x[2], &x[3]);
-    sincos(x[2], &st, &ct);
+    rsincos(x[2], &st, &ct);
   } else {
     x[1] = wx;
     x[2] = wy;
@@ -1114,7 +1131,7 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
       }
     }
   } else {  // sphere.rs:141-150: static emitter
-    stationary_velocity<G>(S, x, ct, u);
+    stationary_velocity<G>(S, x, u);
   }
   double em = inner<G>(S, x, st, ct, u, p);
   double sig0 = signature0<G>();
@@ -1211,7 +1228,8 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
       th = rem_euclid(y[2], PI);
       ph = rem_euclid(y[3] + PI, TWO_PI) - PI;
-      sincos(y[2], &st, &ct);
+      if constexpr (G == GRT_GEOM_SCHWARZSCHILD) st = rsin(y[2]);  // inner_product: sin only
+      else rsincos(y[2], &st, &ct);
     } else {
       double rr;
       cart_to_sph(y[1], y[2], y[3], &rr, &th, &ph);
@@ -1219,7 +1237,7 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     double u = (PI + ph) / TWO_PI;
     double v = th / PI;
     double vel[4], p[4];
-    stationary_velocity<G>(S, y, ct, vel);
+    stationary_velocity<G>(S, y, vel);
     momentum<G>(S, rc, y, p);
     double em = inner<G>(S, y, st, ct, vel, p);
     double sig0 = signature0<G>();

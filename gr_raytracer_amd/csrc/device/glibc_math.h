@@ -1,4 +1,4 @@
-// glibc_math.h — device pow() that returns glibc's bits.
+// glibc_math.h — device pow(), sin(), cos(), sincos() that return glibc's bits.
 //
 // The reference calls f64::powf, i.e. glibc's pow.  On x86-64 with FMA+AVX2 (every
 // machine the reference plausibly runs on, including this image and the GPU boxes),
@@ -112,6 +112,211 @@ GRT_GLIBC_FN bool pow_fast(double x, double y, double* out) {
   const double scale = as_f64(sbits);
   *out = fma_(t, scale, scale);
   return true;
+}
+
+
+// ---------------------------------------------------------------- sin / cos ----
+// glibc 2.35 __sin_fma / __cos_fma (sysdeps/ieee754/dbl-64/s_sin.c, the IBM accurate
+// mathematical library, built with FMA contraction).  do_sin / do_cos / TAYLOR_SIN /
+// reduce_sincos below follow the disassembled FMA variant: each fma_() is one
+// vfmadd/vfnmadd/vfmsub of __sin_fma / __cos_fma.  Covers |x| < 105414350 (the range
+// before glibc's __branred large-argument reduction); the caller falls back beyond.
+
+GRT_GLIBC_FN double copysign_(double mag, double sgn) {
+  return as_f64((as_u64(mag) & 0x7fffffffffffffffull) | (as_u64(sgn) & 0x8000000000000000ull));
+}
+GRT_GLIBC_FN double fabs_(double x) { return as_f64(as_u64(x) & 0x7fffffffffffffffull); }
+
+// TAYLOR_SIN (xx = a*a): a + ((POLY(xx) * a - 0.5 * da) * xx + da)
+GRT_GLIBC_FN double taylor_sin(double a, double da) {
+  const double xx = a * a;
+  const double poly = fma_(fma_(fma_(fma_(S5, xx, S4), xx, S3), xx, S2), xx, S1);
+  const double t = fma_(xx, fma_(poly, a, -(0.5 * da)), da);
+  return a + t;
+}
+
+// do_sin (x, dx): sin(x + dx)
+GRT_GLIBC_FN double do_sin(double x, double dx) {
+  if (fabs_(x) < TAYLOR_MAX) return taylor_sin(x, dx);
+  if (!(x > 0.0)) dx = -dx;
+  const double u = BIG + fabs_(x);
+  const double xr = fabs_(x) - (u - BIG);
+  const int k = (int)((uint32_t)as_u64(u) << 2);
+  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double xx = xr * xr;
+  const double s = xr + fma_(xr * xx, fma_(xx, SN5, SN3), dx);
+  const double c = fma_(xr, dx, xx * fma_(xx, fma_(xx, CS6, CS4), CS2));
+  const double cor = fma_(s, cs, fma_(-c, sn, fma_(s, ccs, ssn)));
+  return copysign_(sn + cor, x);
+}
+
+// do_cos (x, dx): cos(x + dx)
+GRT_GLIBC_FN double do_cos(double x, double dx) {
+  if (x < 0.0) dx = -dx;
+  const double u = BIG + fabs_(x);
+  const double xr = (fabs_(x) - (u - BIG)) + dx;
+  const int k = (int)((uint32_t)as_u64(u) << 2);
+  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double xx = xr * xr;
+  const double s = fma_(xr * xx, fma_(xx, SN5, SN3), xr);
+  const double c = xx * fma_(xx, fma_(xx, CS6, CS4), CS2);
+  const double cor = fma_(-s, sn, fma_(-c, cs, fma_(-s, ssn, ccs)));
+  return cs + cor;
+}
+
+// reduce_sincos: x = n * pi/2 + (a + da), |x| < 105414350
+GRT_GLIBC_FN int reduce_sincos(double x, double* a, double* da) {
+  const double t = fma_(x, HPINV, TOINT);
+  const double xn = t - TOINT;
+  const double y = fma_(-xn, MP2, fma_(-xn, MP1, x));
+  const int n = (int)((uint32_t)as_u64(t) & 3u);
+  const double t2 = fma_(-xn, PP3, y);
+  double db = fma_(-PP3, xn, y - t2);
+  const double b = fma_(-xn, PP4, t2);
+  db = db + fma_(-xn, PP4, t2 - b);
+  *a = b;
+  *da = db;
+  return n;
+}
+
+GRT_GLIBC_FN double do_sincos(double a, double da, int n) {
+  const double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+  return (n & 2) ? -r : r;
+}
+
+// Returns true and sin(x) in *out for |x| < 105414350 (glibc's bits).
+GRT_GLIBC_FN bool sin_fast(double x, double* out) {
+  const uint32_t k = (uint32_t)(as_u64(x) >> 32) & 0x7fffffffu;
+  if (k < 0x3e500000u) {
+    *out = x;
+  } else if (k < 0x3feb6000u) {
+    *out = do_sin(x, 0.0);
+  } else if (k < 0x400368fdu) {
+    const double t = HP0 - fabs_(x);
+    *out = copysign_(do_cos(t, HP1), x);
+  } else if (k < 0x419921fbu) {
+    double a, da;
+    const int n = reduce_sincos(x, &a, &da);
+    *out = do_sincos(a, da, n);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// Returns true and cos(x) in *out for |x| < 105414350 (glibc's bits).
+GRT_GLIBC_FN bool cos_fast(double x, double* out) {
+  const uint32_t k = (uint32_t)(as_u64(x) >> 32) & 0x7fffffffu;
+  if (k < 0x3e400000u) {
+    *out = 1.0;
+  } else if (k < 0x3feb6000u) {
+    *out = do_cos(x, 0.0);
+  } else if (k < 0x400368fdu) {
+    const double y = HP0 - fabs_(x);
+    const double a = y + HP1;
+    const double da = (y - a) + HP1;
+    *out = do_sin(a, da);
+  } else if (k < 0x419921fbu) {
+    double a, da;
+    const int n = reduce_sincos(x, &a, &da);
+    *out = do_sincos(a, da, n + 1);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------- sincos ----
+// glibc 2.35 __sincos (sysdeps/ieee754/dbl-64/s_sincos.c).  It has no ifunc: the
+// baseline x86-64 build runs, i.e. the same IBM routines as sin/cos but WITHOUT FMA
+// contraction.  Compilers fuse sin(x) and cos(x) of one operand into this call (LLVM's
+// sincos libcall combine in the reference's Rust build, GCC's cse_sincos in the
+// oracle), so wherever the reference evaluates both, the device must call this one.
+// The *_nf helpers are s_sin.c's inline functions evaluated as written (device code is
+// compiled with -ffp-contract=off).
+
+GRT_GLIBC_FN double taylor_sin_nf(double a, double da) {
+  const double xx = a * a;
+  const double poly = (((S5 * xx + S4) * xx + S3) * xx + S2) * xx + S1;
+  const double t = ((poly * a - 0.5 * da) * xx + da);
+  return a + t;
+}
+
+GRT_GLIBC_FN double do_sin_nf(double x, double dx) {
+  if (fabs_(x) < TAYLOR_MAX) return taylor_sin_nf(x, dx);
+  if (x <= 0.0) dx = -dx;
+  const double u = BIG + fabs_(x);
+  const double xr = fabs_(x) - (u - BIG);
+  const int k = (int)((uint32_t)as_u64(u) << 2);
+  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double xx = xr * xr;
+  const double s = xr + (dx + xr * xx * (SN3 + xx * SN5));
+  const double c = xr * dx + xx * (CS2 + xx * (CS4 + xx * CS6));
+  const double cor = (ssn + s * ccs - sn * c) + cs * s;
+  return copysign_(sn + cor, x);
+}
+
+GRT_GLIBC_FN double do_cos_nf(double x, double dx) {
+  if (x < 0.0) dx = -dx;
+  const double u = BIG + fabs_(x);
+  const double xr = fabs_(x) - (u - BIG) + dx;
+  const int k = (int)((uint32_t)as_u64(u) << 2);
+  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double xx = xr * xr;
+  const double s = xr + xr * xx * (SN3 + xx * SN5);
+  const double c = xx * (CS2 + xx * (CS4 + xx * CS6));
+  const double cor = (ccs - s * ssn - cs * c) - sn * s;
+  return cs + cor;
+}
+
+GRT_GLIBC_FN int reduce_sincos_nf(double x, double* a, double* da) {
+  const double t = (x * HPINV + TOINT);
+  const double xn = t - TOINT;
+  const double y = (x - xn * MP1) - xn * MP2;
+  const int n = (int)((uint32_t)as_u64(t) & 3u);
+  double t1 = xn * PP3;
+  const double t2 = y - t1;
+  double db = (y - t2) - t1;
+  t1 = xn * PP4;
+  const double b = t2 - t1;
+  db += (t2 - b) - t1;
+  *a = b;
+  *da = db;
+  return n;
+}
+
+GRT_GLIBC_FN double do_sincos_nf(double a, double da, int n) {
+  const double r = (n & 1) ? do_cos_nf(a, da) : do_sin_nf(a, da);
+  return (n & 2) ? -r : r;
+}
+
+// Returns true and (sin x, cos x) for |x| < 105414350 (glibc sincos's bits).
+GRT_GLIBC_FN bool sincos_fast(double x, double* sinx, double* cosx) {
+  const uint32_t k = (uint32_t)(as_u64(x) >> 32) & 0x7fffffffu;
+  if (k < 0x400368fdu) {
+    if (k < 0x3e400000u) {
+      *sinx = x;
+      *cosx = 1.0;
+    } else if (k < 0x3feb6000u) {
+      *sinx = do_sin_nf(x, 0.0);
+      *cosx = do_cos_nf(x, 0.0);
+    } else {
+      const double y = HP0 - fabs_(x);
+      const double a = y + HP1;
+      const double da = (y - a) + HP1;
+      *sinx = copysign_(do_cos_nf(y, HP1), x);
+      *cosx = do_sin_nf(a, da);
+    }
+    return true;
+  }
+  if (k < 0x419921fbu) {
+    double a, da;
+    const int n = reduce_sincos_nf(x, &a, &da);
+    *sinx = do_sincos_nf(a, da, n);
+    *cosx = do_sincos_nf(a, da, n + 1);
+    return true;
+  }
+  return false;
 }
 
 }  // namespace glibc

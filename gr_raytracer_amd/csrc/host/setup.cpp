@@ -477,8 +477,9 @@ int camera_build(int geometry, double radius, double a, const double position[4]
   out->cols = cols;
   out->spatial_signature = -sig0(g);  // signature[3]
   out->spatial_handedness = spatial_handedness(g, pos, T);
-  out->sin_theta = std::sin(pos[2]);
-  out->cos_theta = std::cos(pos[2]);
+  // the KerrBL per-ray constants use sin and cos of this one theta (kerr_bl.rs:505-577):
+  // the reference's compiled code evaluates them with one glibc sincos() call
+  ::sincos(pos[2], &out->sin_theta, &out->cos_theta);
   return 0;
 }
 

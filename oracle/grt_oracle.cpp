@@ -149,9 +149,22 @@ static inline double controller_pow(double x, double e) {
   if (g_libm_probe & 2) return std::nextafter(p, -INFINITY);
   return p;
 }
-static inline double rhs_sin(double x) {
-  double v = std::sin(x);
-  return (g_libm_probe & 4) ? std::nextafter(v, INFINITY) : v;
+// Which glibc entry point each site calls, as the reference's compiled code does:
+// LLVM fuses f64::sin and f64::cos of one operand in one function into a single
+// sincos() libcall, and glibc 2.35's sincos is the baseline (non-FMA) build while
+// sin / cos / pow are the ifunc'd FMA builds -- their last bits differ.  The oracle
+// spells the choice out (g_sincos / g_sin) and is compiled with -fno-builtin-sin
+// -fno-builtin-cos -fno-builtin-sincos so GCC does not fuse on its own.
+static inline void g_sincos(double x, double* s, double* c) { ::sincos(x, s, c); }
+static inline double g_sin(double x) { return ::sin(x); }
+static inline double g_cos(double x) { return ::cos(x); }
+// the RHS's sin/cos pair, with probe bit 4 (sin one ulp up, cos one ulp down)
+static inline void rhs_sincos(double x, double* s, double* c) {
+  g_sincos(x, s, c);
+  if (g_libm_probe & 4) {
+    *s = std::nextafter(*s, INFINITY);
+    *c = std::nextafter(*c, -INFINITY);
+  }
 }
 // probe bits 8 / 16: shading angles (atan2 / acos of hit points and of the final
 // direction, which feed texture coordinates) one ulp up / down
@@ -159,10 +172,6 @@ static inline double shade_angle(double v) {
   if (g_libm_probe & 8) return std::nextafter(v, INFINITY);
   if (g_libm_probe & 16) return std::nextafter(v, -INFINITY);
   return v;
-}
-static inline double rhs_cos(double x) {
-  double v = std::cos(x);
-  return (g_libm_probe & 4) ? std::nextafter(v, -INFINITY) : v;
 }
 
 // spherical_coordinates_helper.rs:5-26
@@ -177,9 +186,12 @@ static Point cartesian_to_spherical(const Point& c) {
 // :28-39
 static Point spherical_to_cartesian(const Point& s) {
   double t = s[0], r = s[1], theta = s[2], phi = s[3];
-  double x = r * std::sin(theta) * std::cos(phi);
-  double y = r * std::sin(theta) * std::sin(phi);
-  double z = r * std::cos(theta);
+  double st, ct, sp, cp;
+  g_sincos(theta, &st, &ct);
+  g_sincos(phi, &sp, &cp);
+  double x = r * st * cp;
+  double y = r * st * sp;
+  double z = r * ct;
   return Point{CS::Cartesian, 0.0, {t, x, y, z}};
 }
 // :44-61
@@ -202,9 +214,12 @@ static Point to_cartesian(const Point& p) {
       return spherical_to_cartesian(p);
     case CS::BoyerLindquist: {
       double a = p.a, t = p[0], r = p[1], theta = p[2], phi = p[3];
-      double x = (r * std::cos(phi) - a * std::sin(phi)) * std::sin(theta);
-      double y = (r * std::sin(phi) + a * std::cos(phi)) * std::sin(theta);
-      double z = r * std::cos(theta);
+      double st, ct, sp, cp;
+      g_sincos(theta, &st, &ct);
+      g_sincos(phi, &sp, &cp);
+      double x = (r * cp - a * sp) * st;
+      double y = (r * sp + a * cp) * st;
+      double z = r * ct;
       return Point{CS::Cartesian, 0.0, {t, x, y, z}};
     }
   }
@@ -346,15 +361,17 @@ struct SchwarzschildSolver : GeodesicSolver {
   void apply(const double* y, double* o) const override {  // :54-80
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
+    double st, ct;
+    rhs_sincos(theta, &st, &ct);
     double a = 1.0 - radius / r;
     double a_prime = radius / (r * r);
     double aprime_over_a = a_prime / a;
     double a_t = -(aprime_over_a)*v_t * v_r;
     double a_r = -0.5 * a * a_prime * v_t * v_t + 0.5 * (aprime_over_a)*v_r * v_r +
-                 a * r * (v_theta * v_theta + v_phi * v_phi * rhs_sin(theta) * rhs_sin(theta));
-    double a_theta = -(2.0 / r) * v_r * v_theta + rhs_sin(theta) * rhs_cos(theta) * v_phi * v_phi;
+                 a * r * (v_theta * v_theta + v_phi * v_phi * st * st);
+    double a_theta = -(2.0 / r) * v_r * v_theta + st * ct * v_phi * v_phi;
     double a_phi =
-        -(2.0 / r) * v_phi * v_r - 2.0 * rhs_cos(theta) / rhs_sin(theta) * v_theta * v_phi;
+        -(2.0 / r) * v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
     o[0] = v_t; o[1] = v_r; o[2] = v_theta; o[3] = v_phi;
     o[4] = a_t; o[5] = a_r; o[6] = a_theta; o[7] = a_phi;
   }
@@ -369,7 +386,7 @@ struct Schwarzschild : Geometry {
     double r = p[1], theta = p[2];  // :90-102
     double a = 1.0 - radius / r;
     return a * v[0] * w[0] - v[1] * w[1] / a - r * r * v[2] * w[2] -
-           r * r * std::sin(theta) * std::sin(theta) * v[3] * w[3];
+           r * r * g_sin(theta) * g_sin(theta) * v[3] * w[3];
   }
   bool inside_horizon(const Point& p) const override {  // :181-183
     return p[1] <= radius + horizon_epsilon;
@@ -552,14 +569,14 @@ struct Kerr : Geometry {
 };
 
 // ---- KerrBL, Boyer-Lindquist with Carter constant (geometry/kerr_bl.rs) ----
-static double bl_sigma(double r, double a, double theta) {  // :62-64
-  double c = std::cos(theta);
-  return r * r + a * a * (c * c);
+static double bl_sigma(double r, double a, double cos_t) {  // :62-64 (cos theta passed in)
+  return r * r + a * a * (cos_t * cos_t);
 }
 static double bl_delta(double r, double r_s, double a) { return r * r - r_s * r + a * a; }
 static Mat4 metric_bl(double r_s, double a, double r, double theta) {  // :253-272
-  double sig = bl_sigma(r, a, theta);
-  double sin_t = std::sin(theta);
+  double sin_t, cos_t;  // sigma's cos and this sin of one theta: one sincos
+  g_sincos(theta, &sin_t, &cos_t);
+  double sig = bl_sigma(r, a, cos_t);
   double sin2 = sin_t * sin_t;
   Mat4 g;
   std::memset(&g, 0, sizeof(g));
@@ -578,7 +595,8 @@ struct KerrBLSolver : GeodesicSolver {
     double r = y[1], theta = y[2], v_r = y[4], v_theta = y[5];
     double del = bl_delta(r, radius, a);
     double p_r = (r * r + a * a) * e - a * l_z;
-    double sin_t = rhs_sin(theta);
+    double sin_t, cos_t;  // geodesic + potential_theta_derivative: one sincos
+    rhs_sincos(theta, &sin_t, &cos_t);
     double sin2 = sin_t * sin_t;
     double dt = (r * r + a * a) / del * p_r + a * (l_z - a * e * sin2);
     double dphi = a / del * p_r + l_z / sin2 - a * e;
@@ -588,7 +606,7 @@ struct KerrBLSolver : GeodesicSolver {
     double carter = le * le + q;
     double dv_r = (4.0 * r * e * p_r2 - (2.0 * r - radius) * carter) / 2.0;
     // potential_theta_derivative :114-118
-    double cos_t = rhs_cos(theta), sin_t2 = rhs_sin(theta);
+    double sin_t2 = sin_t;
     double dv_theta = (-2.0 * a * a * e * e * cos_t * sin_t2 +
                        2.0 * l_z * l_z * cos_t / (sin_t2 * (sin_t2 * sin_t2))) /
                       2.0;
@@ -606,7 +624,8 @@ struct KerrBLSolver : GeodesicSolver {
     double le = l_z - a * e;
     double r_pot = p_r * p_r - del * (le * le + q);
     // potential_theta :101-105
-    double cos_t = std::cos(theta), sin_t = std::sin(theta);
+    double cos_t, sin_t;
+    g_sincos(theta, &sin_t, &cos_t);
     double th_pot = q + a * a * e * e * cos_t * cos_t - l_z * l_z * cos_t * cos_t / (sin_t * sin_t);
     y[0] = t; y[1] = r; y[2] = theta; y[3] = phi;
     y[4] = sign_r * std::sqrt(std::fmax(r_pot, 0.0));
@@ -616,8 +635,9 @@ struct KerrBLSolver : GeodesicSolver {
   FourVector momentum_from_state(const double* y) const override {  // :225-249
     double r = y[1], theta = y[2], v_r = y[4], v_theta = y[5];
     double del = bl_delta(r, radius, a);
-    double sig = bl_sigma(r, a, theta);
-    double s = std::sin(theta);
+    double s, c;  // sigma's cos and this sin: one sincos
+    g_sincos(theta, &s, &c);
+    double sig = bl_sigma(r, a, c);
     double sin2 = s * s;
     double p_r_term = (r * r + a * a) * e - a * l_z;
     double dt = (r * r + a * a) / del * p_r_term + a * (l_z - a * e * sin2);
@@ -651,7 +671,8 @@ struct KerrBL : Geometry {
     double pc[4];
     mat_vec(g, ray.momentum.v, pc);
     double e = -pc[0], l_z = pc[3], p_theta = pc[2];
-    double cos_t = std::cos(theta), sin_t = std::sin(theta);
+    double cos_t, sin_t;
+    g_sincos(theta, &sin_t, &cos_t);
     double sin2 = sin_t * sin_t;
     double q = p_theta * p_theta + cos_t * cos_t * (l_z * l_z / std::fmax(sin2, 1e-28) - a * a * e * e);
     KerrBLSolver* s = new KerrBLSolver();
@@ -667,7 +688,7 @@ struct KerrBL : Geometry {
   }
   FourVector stationary_velocity(const Point& p) const override {  // :362-371
     double r = p[1], theta = p[2];
-    double sig = bl_sigma(r, a, theta);
+    double sig = bl_sigma(r, a, g_cos(theta));  // sigma alone: a lone cos()
     double ut = 1.0 / std::sqrt(1.0 - radius * r / sig);
     return FourVector{CS::BoyerLindquist, {ut, 0.0, 0.0, 0.0}};
   }
@@ -990,8 +1011,10 @@ static bool disc_intersects(const grt_object_desc& o, const Point& ys, const Poi
     double vx = ip.x - 0.0, vy = ip.y - 0.0;
     double phi = shade_angle(std::atan2(vy, vx));
     double r = (std::sqrt(rr) - rin) / (rout - rin);
-    out->u = 0.5 + 0.5 * r * std::cos(phi);
-    out->v = 0.5 + 0.5 * r * std::sin(phi);
+    double sp, cp;
+    g_sincos(phi, &sp, &cp);
+    out->u = 0.5 + 0.5 * r * cp;
+    out->v = 0.5 + 0.5 * r * sp;
     out->point = Point{CS::Cartesian, 0.0, {0.0, ip.x, ip.y, ip.z}};
     out->t = t;
     return true;

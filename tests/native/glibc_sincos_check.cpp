@@ -1,0 +1,38 @@
+// Host build of glibc_math.h's sincos_fast checked against glibc sincos, bit for bit.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+
+#include "glibc_math.h"
+
+extern "C" void sincos(double, double*, double*);
+
+int main(int argc, char** argv) {
+  const int mode = atoi(argv[1]);
+  const long n = atol(argv[2]);
+  std::mt19937_64 rng(4242 + mode);
+  std::uniform_real_distribution<double> u01(0.0, 1.0);
+  long fast = 0, bad = 0;
+  for (long k = 0; k < n; ++k) {
+    double x;
+    switch (mode) {
+      case 0: x = (u01(rng) * 1.4 - 0.2) * 3.141592653589793; break;
+      case 1: x = (u01(rng) - 0.5) * 40.0; break;
+      case 2: x = std::ldexp(u01(rng) - 0.5, (int)(rng() % 60) - 40); break;
+      case 3: x = 1.5707963267948966 + (u01(rng) - 0.5) * 1e-6; break;
+      default: x = (u01(rng) - 0.5) * 2e8;
+    }
+    double gs, gc, ws, wc;
+    if (!grt::glibc::sincos_fast(x, &gs, &gc)) continue;
+    ++fast;
+    sincos(x, &ws, &wc);
+    if (memcmp(&gs, &ws, 8) != 0 || memcmp(&gc, &wc, 8) != 0) {
+      if (bad < 5) printf("# mismatch x=%a got=(%a,%a) want=(%a,%a)\n", x, gs, gc, ws, wc);
+      ++bad;
+    }
+  }
+  printf("%ld %ld %ld\n", n, fast, bad);
+  return 0;
+}

@@ -38,3 +38,32 @@ def test_tables_match_the_installed_libm():
     gen = subprocess.run(["python3", str(ROOT / "tools" / "gen_glibc_tables.py")], check=True, capture_output=True,
                          text=True).stdout
     assert gen == (DEV / "glibc_tables.h").read_text()
+
+
+TRIG_MODES = {0: "ray theta", 1: "several periods", 2: "magnitudes 2^-41..2^19", 3: "near pi/2",
+              4: "up to the reduction limit"}
+
+
+def _build(tmp_path_factory, name, extra=()):
+    exe = tmp_path_factory.mktemp(name) / name
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", *extra, "-I", str(DEV),
+                    str(ROOT / "tests" / "native" / f"{name}.cpp"), "-o", str(exe)], check=True)
+    return exe
+
+
+@pytest.fixture(scope="module")
+def trig_checkers(tmp_path_factory):
+    # -fno-builtin: sin(x) and cos(x) must reach glibc's sin / cos, not a fused sincos
+    return (_build(tmp_path_factory, "glibc_trig_check", ("-fno-builtin-sin", "-fno-builtin-cos")),
+            _build(tmp_path_factory, "glibc_sincos_check"))
+
+
+@pytest.mark.parametrize("mode", sorted(TRIG_MODES))
+def test_device_sin_cos_sincos_are_bit_identical_to_glibc(trig_checkers, mode):
+    """sin_fast / cos_fast == glibc sin / cos (FMA ifunc builds); sincos_fast == glibc
+    sincos (baseline build), on |x| < 105414350."""
+    for exe in trig_checkers:
+        out = subprocess.run([str(exe), str(mode), "300000"], check=True, capture_output=True, text=True).stdout
+        n, fast, bad = map(int, out.strip().splitlines()[-1].split())
+        assert bad == 0, (exe.name, out)
+        assert fast == n, (exe.name, TRIG_MODES[mode], fast, n)
