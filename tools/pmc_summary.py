@@ -1,0 +1,68 @@
+"""Summarise the rocprofv3 --pmc passes of tools/run_pmc.sh for the integrate kernel.
+
+usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<tag>_pmc.json
+Counter values are summed over the rows of each dispatch of grt::integrate_kernel<1>
+(one C2 frame per dispatch) and reported per launch.  FETCH_SIZE (KB) is doubled per
+the gfx950 correction in MI355X_MICROARCH.md; WRITE_SIZE (KB) is taken as is.
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+KERNEL = "grt::integrate_kernel<1>"
+
+
+def load(pass_dir):
+    vals = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
+    dur = {}
+    for f in glob.glob(str(Path(pass_dir) / "**" / "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if KERNEL not in row["Kernel_Name"]:
+                    continue
+                d = row["Dispatch_Id"]
+                vals[row["Counter_Name"]][d] += float(row["Counter_Value"])
+                dur[d] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
+    return vals, dur
+
+
+def main():
+    src, dst = Path(sys.argv[1]), Path(sys.argv[2])
+    counters, kernel_ms = {}, {}
+    for p in ("fetch", "write", "valu", "busy"):
+        vals, dur = load(src / p)
+        for c, per in vals.items():
+            counters[c] = sum(per.values()) / len(per)
+        if dur:
+            kernel_ms[p] = sum(dur.values()) / len(dur)
+    fetch_b = counters.get("FETCH_SIZE", 0.0) * 1024 * 2
+    write_b = counters.get("WRITE_SIZE", 0.0) * 1024
+    out = {
+        "kernel": f"{KERNEL} (Schwarzschild), one C2 frame (1500x1500, 2.25M rays)",
+        "source": "rocprofv3 --kernel-trace --pmc <one counter group per pass>, tools/run_pmc.sh",
+        "counters": counters,
+        "kernel_ms_per_pass": kernel_ms,
+        "fetch_bytes_corrected": fetch_b,
+        "write_bytes": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "notes": "FETCH_SIZE (KB) doubled per the gfx950 correction; WRITE_SIZE (KB) taken as is.",
+    }
+    c = counters
+    if c.get("SQ_INSTS_VALU"):
+        f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+        out["valu_f64_fraction"] = f64 / c["SQ_INSTS_VALU"]
+    if c.get("SQ_WAVE_CYCLES"):
+        out["active_valu_over_wave_cycles"] = c.get("SQ_ACTIVE_INST_VALU", 0.0) / c["SQ_WAVE_CYCLES"]
+        out["wait_inst_any_over_wave_cycles"] = c.get("SQ_WAIT_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+    if c.get("SQ_ACTIVE_INST_VALU") and c.get("SQ_THREAD_CYCLES_VALU"):
+        out["lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
+    dst.write_text(json.dumps(out, indent=1) + "\n")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
