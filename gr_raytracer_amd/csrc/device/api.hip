@@ -185,6 +185,11 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   ds.cel_lo2 = ds.max_radius_sq * (1.0 - 1e-9);
   ds.cel_hi2 = ds.max_radius_sq * (1.0 + 1e-9);
   if (!std::isfinite(ds.far_a) || !std::isfinite(ds.max_radius_sq)) ds.far_ok = 0;
+  {
+    int ex = 0;
+    std::frexp(d.radius, &ex);
+    ds.div_share = (std::fpclassify(d.radius) == FP_NORMAL && ex > -500 && ex < 500) ? 1 : 0;
+  }
   const grt_camera_desc& c = d.camera;
   for (int k = 0; k < 4; ++k) {
     ds.cam.pos[k] = c.position[k];

@@ -61,7 +61,7 @@ struct DevScene {
   // far-field filter: Cartesian radius of a state is within [r, r + far_a]; the
   // celestial test |x|^2 > max_radius^2 is decided from r outside [cel_lo2, cel_hi2]
   int32_t far_ok;         // geometry has a curvilinear chart (Schwarzschild / KerrBL)
-  int32_t _pad2;
+  int32_t div_share;      // radius is a moderate normal: x / r divisions may share 1 / r
   double far_a, cel_lo2, cel_hi2;
   DevCamera cam;
   DevTexture celestial;

@@ -27,12 +27,19 @@
 
 #include "grt_api.h"
 #include "dev_scene.h"
+#ifndef GRT_GLIBC_LDS
+#define GRT_GLIBC_LDS 1  // glibc tables staged in LDS per workgroup (measured -1..2%)
+#endif
 #include "glibc_math.h"
 #include "kernels.h"
 
 namespace grt {
 
 #define GDEV __device__ __forceinline__
+
+#ifndef GRT_SHARED_DIV
+#define GRT_SHARED_DIV 1
+#endif
 
 // f64::powf == glibc pow: bit-exact on glibc's fast path, OCML outside it.
 GDEV double rpow(double x, double y) {
@@ -55,6 +62,29 @@ GDEV double rcos(double x) {
   double r;
   if (glibc::cos_fast(x, &r)) return r;
   return cos(x);
+}
+
+// x1 / y and x2 / y with one reciprocal refinement.  This is the compiler's own IEEE f64
+// division expansion (div_scale, rcp, 2 Newton steps, div_fmas, div_fixup -- identical
+// instructions), with the y-only part shared.  The shared part is v_div_scale(y, y, x),
+// whose result depends on x only when |x| is extreme (exponent gap >= 768, x/y
+// denormal, or exp(x) <= 53); the host enables this (DevScene::div_share) only when
+// both numerators are normal with |exponent| < 500, where it cannot.  Every quotient
+// is therefore bit-identical to x / y.
+GDEV void div2_same_den(double x1, double x2, double y, double* q1, double* q2) {
+  bool f0, f1, f2;
+  const double ds0 = __builtin_amdgcn_div_scale(x1, y, false, &f0);
+  const double rcp = __builtin_amdgcn_rcp(ds0);
+  const double fma0 = __builtin_fma(-ds0, rcp, 1.0);
+  const double fma1 = __builtin_fma(rcp, fma0, rcp);
+  const double fma2 = __builtin_fma(-ds0, fma1, 1.0);
+  const double fma3 = __builtin_fma(fma1, fma2, fma1);
+  const double n1 = __builtin_amdgcn_div_scale(x1, y, true, &f1);
+  const double m1 = n1 * fma3;
+  *q1 = __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(__builtin_fma(-ds0, m1, n1), fma3, m1, f1), y, x1);
+  const double n2 = __builtin_amdgcn_div_scale(x2, y, true, &f2);
+  const double m2 = n2 * fma3;
+  *q2 = __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(__builtin_fma(-ds0, m2, n2), fma3, m2, f2), y, x2);
 }
 
 constexpr double PI = 3.14159265358979323846;
@@ -267,10 +297,19 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
     double st, ct;
     rsincos(theta, &st, &ct);
-    double a = 1.0 - radius / r;
+    double radius_over_r, two_over_r;
+#if GRT_SHARED_DIV
+    if (S.div_share) {
+      div2_same_den(radius, 2.0, r, &radius_over_r, &two_over_r);
+    } else
+#endif
+    {
+      radius_over_r = radius / r;
+      two_over_r = 2.0 / r;
+    }
+    double a = 1.0 - radius_over_r;
     double a_prime = radius / (r * r);
     double aprime_over_a = a_prime / a;
-    double two_over_r = 2.0 / r;
     o[0] = v_t;
     o[1] = v_r;
     o[2] = v_theta;
@@ -881,6 +920,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     const DevScene* __restrict__ Sp, WorkList wl, Workspace ws, unsigned long long* __restrict__ counter,
     unsigned long long* __restrict__ stats) {
   const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr uint64_t CHUNK = 64;
@@ -1175,6 +1215,7 @@ template <int G>
 __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__ Sp, Workspace ws, Outputs out,
                                                     unsigned long long* __restrict__ stats) {
   const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before the early return
   const uint64_t n = ws.n;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n) return;

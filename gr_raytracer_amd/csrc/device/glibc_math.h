@@ -37,6 +37,33 @@
 namespace grt {
 namespace glibc {
 
+// Table access.  On the device the lookups are per-lane gathers; from __constant__
+// memory they go through L1/L2 and their latency stalls the two resident waves, so a
+// kernel can stage the tables in LDS once per workgroup (tables_to_lds) and build with
+// GRT_GLIBC_LDS.  Same values either way.
+#if defined(__HIPCC__) && defined(GRT_GLIBC_LDS) && GRT_GLIBC_LDS
+__shared__ double lds_sincos[440];
+__shared__ double lds_powlog[128 * 3];
+__shared__ uint64_t lds_exp[256];
+#define GRT_SINCOS(k) lds_sincos[k]
+#define GRT_POWLOG(i, j) lds_powlog[(i) * 3 + (j)]
+#define GRT_EXPTAB(k) lds_exp[k]
+// every thread of the block must call this before any lookup
+__device__ static inline void tables_to_lds() {
+  for (unsigned i = threadIdx.x; i < 440u; i += blockDim.x) lds_sincos[i] = SINCOS_TAB[i];
+  for (unsigned i = threadIdx.x; i < 384u; i += blockDim.x) lds_powlog[i] = POW_LOG_TAB[i / 3][i % 3];
+  for (unsigned i = threadIdx.x; i < 256u; i += blockDim.x) lds_exp[i] = EXP_TAB[i];
+  __syncthreads();
+}
+#else
+#define GRT_SINCOS(k) SINCOS_TAB[k]
+#define GRT_POWLOG(i, j) POW_LOG_TAB[i][j]
+#define GRT_EXPTAB(k) EXP_TAB[k]
+#if defined(__HIPCC__)
+__device__ static inline void tables_to_lds() {}
+#endif
+#endif
+
 GRT_GLIBC_FN uint64_t as_u64(double x) {
   uint64_t u;
   memcpy(&u, &x, 8);
@@ -67,7 +94,7 @@ GRT_GLIBC_FN bool pow_fast(double x, double y, double* out) {
   const uint64_t iz = ix - (tmp & 0xfff0000000000000ull);
   const double z = as_f64(iz);
   const double kd = (double)k;
-  const double invc = POW_LOG_TAB[i][0], logc = POW_LOG_TAB[i][1], logctail = POW_LOG_TAB[i][2];
+  const double invc = GRT_POWLOG(i, 0), logc = GRT_POWLOG(i, 1), logctail = GRT_POWLOG(i, 2);
   const double t1 = fma_(kd, POW_LN2HI, logc);
   const double r = fma_(z, invc, -1.0);
   const double ar = r * POW_A[0];
@@ -101,8 +128,8 @@ GRT_GLIBC_FN bool pow_fast(double x, double y, double* out) {
   re = fma_(kn, EXP_NEGLN2LON, re);
   const uint32_t idx = (uint32_t)(ki & 127u) * 2u;
   const uint64_t top = ki << 45;
-  const double tail = as_f64(EXP_TAB[idx]);
-  const uint64_t sbits = EXP_TAB[idx + 1] + top;
+  const double tail = as_f64(GRT_EXPTAB(idx));
+  const uint64_t sbits = GRT_EXPTAB(idx + 1) + top;
   re = elo + re;
   const double p23 = fma_(re, EXP_C3, EXP_C2);
   const double tr = re + tail;
@@ -142,7 +169,7 @@ GRT_GLIBC_FN double do_sin(double x, double dx) {
   const double u = BIG + fabs_(x);
   const double xr = fabs_(x) - (u - BIG);
   const int k = (int)((uint32_t)as_u64(u) << 2);
-  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double sn = GRT_SINCOS(k), ssn = GRT_SINCOS(k + 1), cs = GRT_SINCOS(k + 2), ccs = GRT_SINCOS(k + 3);
   const double xx = xr * xr;
   const double s = xr + fma_(xr * xx, fma_(xx, SN5, SN3), dx);
   const double c = fma_(xr, dx, xx * fma_(xx, fma_(xx, CS6, CS4), CS2));
@@ -156,7 +183,7 @@ GRT_GLIBC_FN double do_cos(double x, double dx) {
   const double u = BIG + fabs_(x);
   const double xr = (fabs_(x) - (u - BIG)) + dx;
   const int k = (int)((uint32_t)as_u64(u) << 2);
-  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double sn = GRT_SINCOS(k), ssn = GRT_SINCOS(k + 1), cs = GRT_SINCOS(k + 2), ccs = GRT_SINCOS(k + 3);
   const double xx = xr * xr;
   const double s = fma_(xr * xx, fma_(xx, SN5, SN3), xr);
   const double c = xx * fma_(xx, fma_(xx, CS6, CS4), CS2);
@@ -248,7 +275,7 @@ GRT_GLIBC_FN double do_sin_nf(double x, double dx) {
   const double u = BIG + fabs_(x);
   const double xr = fabs_(x) - (u - BIG);
   const int k = (int)((uint32_t)as_u64(u) << 2);
-  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double sn = GRT_SINCOS(k), ssn = GRT_SINCOS(k + 1), cs = GRT_SINCOS(k + 2), ccs = GRT_SINCOS(k + 3);
   const double xx = xr * xr;
   const double s = xr + (dx + xr * xx * (SN3 + xx * SN5));
   const double c = xr * dx + xx * (CS2 + xx * (CS4 + xx * CS6));
@@ -261,7 +288,7 @@ GRT_GLIBC_FN double do_cos_nf(double x, double dx) {
   const double u = BIG + fabs_(x);
   const double xr = fabs_(x) - (u - BIG) + dx;
   const int k = (int)((uint32_t)as_u64(u) << 2);
-  const double sn = SINCOS_TAB[k], ssn = SINCOS_TAB[k + 1], cs = SINCOS_TAB[k + 2], ccs = SINCOS_TAB[k + 3];
+  const double sn = GRT_SINCOS(k), ssn = GRT_SINCOS(k + 1), cs = GRT_SINCOS(k + 2), ccs = GRT_SINCOS(k + 3);
   const double xx = xr * xr;
   const double s = xr + xr * xx * (SN3 + xx * SN5);
   const double c = xx * (CS2 + xx * (CS4 + xx * CS6));
