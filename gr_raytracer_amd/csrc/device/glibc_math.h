@@ -270,7 +270,13 @@ GRT_GLIBC_FN double taylor_sin_nf(double a, double da) {
 }
 
 GRT_GLIBC_FN double do_sin_nf(double x, double dx) {
+#if defined(GRT_GLIBC_BRANCHLESS) && GRT_GLIBC_BRANCHLESS
+  // both of glibc's forms, then a select: the same value as the branch, without the
+  // divergent branch when a wave mixes |x| < 0.126 and |x| >= 0.126 lanes
+  const double taylor = taylor_sin_nf(x, dx);
+#else
   if (fabs_(x) < TAYLOR_MAX) return taylor_sin_nf(x, dx);
+#endif
   if (x <= 0.0) dx = -dx;
   const double u = BIG + fabs_(x);
   const double xr = fabs_(x) - (u - BIG);
@@ -280,7 +286,11 @@ GRT_GLIBC_FN double do_sin_nf(double x, double dx) {
   const double s = xr + (dx + xr * xx * (SN3 + xx * SN5));
   const double c = xr * dx + xx * (CS2 + xx * (CS4 + xx * CS6));
   const double cor = (ssn + s * ccs - sn * c) + cs * s;
+#if defined(GRT_GLIBC_BRANCHLESS) && GRT_GLIBC_BRANCHLESS
+  return fabs_(x) < TAYLOR_MAX ? taylor : copysign_(sn + cor, x);
+#else
   return copysign_(sn + cor, x);
+#endif
 }
 
 GRT_GLIBC_FN double do_cos_nf(double x, double dx) {
