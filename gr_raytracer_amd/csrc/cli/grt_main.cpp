@@ -157,7 +157,12 @@ int main(int argc, char** argv) {
     ok = grt_host::hdr_encode_rgb(filename, rgb.data(), w, h, err);
   } else {
     std::vector<uint8_t> rgb((size_t)w * h * 3);
-    grt_xyz_to_srgb8(xyza.data(), (size_t)w * h, opts.tone_mapping, 1.0, rgb.data());
+    // output stage on the GPU (color.rs:204-298 via output.hip), exposure 1 as in
+    // render_section (raytracer.rs:485)
+    if (grt_xyz_to_srgb8_device(device, xyza.data(), (size_t)w * h, opts.tone_mapping, 1.0, rgb.data())) {
+      std::fprintf(stderr, "Error: %s\n", grt_last_error());
+      return 1;
+    }
     ok = grt_host::png_encode_rgb(filename, rgb.data(), w, h, err);
   }
   if (!ok) {

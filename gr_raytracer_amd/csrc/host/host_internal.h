@@ -27,6 +27,8 @@ int blackbody_lut(uint32_t n, double* log_t, double* xyz);
 double inv_compand_srgb(double u);
 void srgb_to_xyza(uint8_t r8, uint8_t g8, uint8_t b8, uint8_t a8, double out[4]);
 int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_t* rgb);
+void linear_max(const double* xyza, size_t n, double exposure, double* max3);
+int tonemap(const double* xyza, size_t n, int tone, double exposure, const double* max3, uint8_t* rgb);
 int stationary(int geometry, double radius, double a, const double position[4], double out[4]);
 int zamo(int geometry, double radius, double a, const double position[4], double out[4]);
 

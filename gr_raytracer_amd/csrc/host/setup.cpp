@@ -712,34 +712,40 @@ static uint8_t to_u8(double v) {  // (x * 255.0).round() as u8 (saturating)
   if (r >= 255.0) return 255;
   return (uint8_t)r;
 }
-int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_t* rgb) {
+static void to_linear(const double* c, double* lin) {  // color.rs:208-223, nalgebra gemv order
   static const double M[3][3] = {{3.2406255, -1.5372080, -0.4986286},
                                  {-0.9689307, 1.8757561, 0.0415175},
                                  {0.0557101, -0.2040211, 1.0569959}};
-  std::vector<double> lin(3 * n);
-  for (size_t i = 0; i < n; ++i) {
-    const double* c = xyza + 4 * i;
-    for (int k = 0; k < 3; ++k) {
-      double s = M[k][0] * c[0];
-      s = M[k][1] * c[1] + s;
-      s = M[k][2] * c[2] + s;
-      lin[3 * i + k] = s;
-    }
+  for (int k = 0; k < 3; ++k) {
+    double s = M[k][0] * c[0];
+    s = M[k][1] * c[1] + s;
+    s = M[k][2] * c[2] + s;
+    lin[k] = s;
   }
+}
+// GlobalLinear's per-channel fold(0.0, f64::max) of (linear * exposure) (color.rs:238-258)
+void linear_max(const double* xyza, size_t n, double exposure, double* max3) {
+  double m[3] = {0.0, 0.0, 0.0};
+  for (size_t i = 0; i < n; ++i) {
+    double lin[3];
+    to_linear(xyza + 4 * i, lin);
+    for (int k = 0; k < 3; ++k) m[k] = std::fmax(m[k], lin[k] * exposure);
+  }
+  for (int k = 0; k < 3; ++k) max3[k] = m[k];
+}
+int tonemap(const double* xyza, size_t n, int tone, double exposure, const double* max3, uint8_t* rgb) {
+  if (tone != GRT_TONE_REINHARD && tone != GRT_TONE_GLOBAL_LINEAR) return -EINVAL;
   double sc = 1.0;
-  if (tone == 1) {  // GlobalLinear
-    double mr = 0.0, mg = 0.0, mb = 0.0;
-    for (size_t i = 0; i < n; ++i) {
-      mr = std::fmax(mr, lin[3 * i] * exposure);
-      mg = std::fmax(mg, lin[3 * i + 1] * exposure);
-      mb = std::fmax(mb, lin[3 * i + 2] * exposure);
-    }
-    double mc = std::fmax(std::fmax(mr, mg), mb);
+  if (tone == GRT_TONE_GLOBAL_LINEAR) {
+    if (!max3) return -EINVAL;
+    double mc = std::fmax(std::fmax(max3[0], max3[1]), max3[2]);
     sc = mc > 0.0 ? 1.0 / mc : 1.0;
   }
   for (size_t i = 0; i < n; ++i) {
-    double c[3] = {lin[3 * i] * exposure, lin[3 * i + 1] * exposure, lin[3 * i + 2] * exposure};
-    if (tone == 0) {
+    double c[3];
+    to_linear(xyza + 4 * i, c);
+    for (int k = 0; k < 3; ++k) c[k] = c[k] * exposure;
+    if (tone == GRT_TONE_REINHARD) {
       double l_in = 0.2126 * c[0] + 0.7152 * c[1] + 0.0722 * c[2];
       if (l_in > 0.0) {
         double l_out = l_in / (1.0 + l_in);
@@ -752,6 +758,11 @@ int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_
     for (int k = 0; k < 3; ++k) rgb[3 * i + k] = to_u8(compand_srgb(std::fmax(c[k], 0.0)));
   }
   return 0;
+}
+int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_t* rgb) {
+  double m[3] = {0.0, 0.0, 0.0};
+  if (tone == GRT_TONE_GLOBAL_LINEAR) linear_max(xyza, n, exposure, m);
+  return tonemap(xyza, n, tone, exposure, m, rgb);
 }
 
 int stationary(int geometry, double radius, double a, const double position[4], double out[4]) {
@@ -822,6 +833,15 @@ void grt_blackbody_xyz(double temperature, double redshift, double out_xyz[3]) {
 }
 void grt_srgb_to_xyza(uint8_t r, uint8_t g, uint8_t b, uint8_t a, double out[4]) {
   grt_host::srgb_to_xyza(r, g, b, a, out);
+}
+void grt_linear_max(const double* xyza, size_t n, double exposure, double max3[3]) {
+  grt_host::linear_max(xyza, n, exposure, max3);
+}
+int grt_tonemap(const double* xyza, size_t n, int32_t tone_mapping, double exposure, const double max3[3],
+                uint8_t* rgb_out) {
+  int rc = grt_host::tonemap(xyza, n, tone_mapping, exposure, max3, rgb_out);
+  if (rc) grt_host::set_error("grt_tonemap: unknown tone mapping or missing maxima");
+  return rc;
 }
 int grt_xyz_to_srgb8(const double* xyza, size_t n, int32_t tone_mapping, double exposure, uint8_t* rgb_out) {
   if (!xyza || !rgb_out) return -EINVAL;

@@ -259,6 +259,21 @@ def srgb_to_xyza(r: int, g: int, b: int, a: int = 255) -> np.ndarray:
     return out
 
 
+def xyz_to_srgb8(xyza, tone_mapping: int = 0, exposure: float = 1.0, device: Optional[int] = None) -> np.ndarray:
+    """Output stage (color.rs:204-298): (n,4) f64 XYZA -> (n,3) u8 sRGB.  device=None
+    runs the host C++ path (grt_xyz_to_srgb8), an ordinal runs the HIP kernels
+    (grt_xyz_to_srgb8_device); both return the reference's bytes."""
+    x = np.ascontiguousarray(xyza, np.float64).reshape(-1, 4)
+    out = np.zeros((x.shape[0], 3), np.uint8)
+    if device is None:
+        L.check(L.lib().grt_xyz_to_srgb8(L.dptr(x), x.shape[0], tone_mapping, exposure, L.ptr(out, C.c_uint8)),
+                "grt_xyz_to_srgb8")
+    else:
+        L.check(L.lib().grt_xyz_to_srgb8_device(device, L.dptr(x), x.shape[0], tone_mapping, exposure,
+                                                 L.ptr(out, C.c_uint8)), "grt_xyz_to_srgb8_device")
+    return out
+
+
 def r_isco(radius: float, a: float) -> float:
     return float(L.lib().grt_r_isco(radius, a))
 

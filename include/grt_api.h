@@ -66,6 +66,9 @@ enum grt_temperature_kind {
 /* scene.rs:25-30 RayClass. */
 enum grt_ray_class { GRT_CLASS_ESCAPED = 0, GRT_CLASS_CAPTURED = 1, GRT_CLASS_HIT = 2 };
 
+/* color.rs:16-21 ToneMappingMethod. */
+enum grt_tone_mapping { GRT_TONE_REINHARD = 0, GRT_TONE_GLOBAL_LINEAR = 1 };
+
 /* Per-pixel status: which RaytracerError (raytracer.rs:20-52) aborted the pixel.
  * A pixel with a non-zero status keeps the reference default {(0,0,0,1), Escaped}
  * (raytracer.rs:204-210, :232-239).  Bit 7 flags are informational. */
@@ -241,7 +244,12 @@ int grt_blackbody_lut(uint32_t n, double* log_t, double* xyz);
 void grt_blackbody_xyz(double temperature, double redshift, double out_xyz[3]);
 /* srgb_to_xyz (color.rs:310-332), alpha := a/255 (CIETristimulus::from_color). */
 void grt_srgb_to_xyza(uint8_t r, uint8_t g, uint8_t b, uint8_t a, double out[4]);
-/* xyz -> tone-mapped sRGB8 (color.rs:204-298), whole buffer. */
+/* xyz -> tone-mapped sRGB8 (color.rs:204-298), whole buffer = grt_linear_max (only for
+ * GlobalLinear) + grt_tonemap.  Split so that a frame spread over several processes
+ * can reduce the three channel maxima (MAX) before mapping its own rows. */
+void grt_linear_max(const double* xyza, size_t n, double exposure, double max3[3]);
+int grt_tonemap(const double* xyza, size_t n, int32_t tone_mapping, double exposure,
+                const double max3[3], uint8_t* rgb_out);
 int grt_xyz_to_srgb8(const double* xyza, size_t n, int32_t tone_mapping, double exposure,
                      uint8_t* rgb_out);
 
@@ -331,6 +339,23 @@ int grt_render_shard(grt_scene* scene, int device, const grt_row_shard* sh, floa
 int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt_row_shard* sh,
                            float* d_xyza, uint8_t* d_class, uint8_t* d_status, double* d_xyza64,
                            uint32_t* d_steps, uint8_t* d_stop, uint64_t* d_stats);
+
+/* ---- device output stage ------------------------------- */
+/* Replaces xyz_to_linear_srgb_buffer + linear_srgb_to_srgb_buffer (color.rs:204-298),
+ * called by Raytracer::render_section for non-HDR files (raytracer.rs:460-497).
+ * GlobalLinear needs the per-channel maxima of (linear sRGB * exposure) over the WHOLE
+ * frame, folded from 0.0 (color.rs:238-258): grt_linear_max_async writes them to
+ * d_max3 (3 doubles, device); a frame split across GPUs allreduces them (MAX) before
+ * grt_tonemap_async.  Byte-identical to the reference (glibc pow restated on device).
+ * d_xyza: n x 4 f64 (the render's xyza64 output); d_rgb: n x 3 u8.  Async on `stream`. */
+int grt_linear_max_async(int device, void* stream, const double* d_xyza, uint64_t n,
+                         double exposure, double* d_max3);
+int grt_tonemap_async(int device, void* stream, const double* d_xyza, uint64_t n,
+                      int32_t tone_mapping, double exposure, const double* d_max3,
+                      uint8_t* d_rgb);
+/* Host buffers in and out, same result as grt_xyz_to_srgb8, computed on `device`. */
+int grt_xyz_to_srgb8_device(int device, const double* xyza, size_t n, int32_t tone_mapping,
+                            double exposure, uint8_t* rgb_out);
 
 /* Kernel launch geometry knobs (persistent grid). 0 = library default. */
 int grt_set_launch_config(int blocks_per_cu, int threads_per_block);

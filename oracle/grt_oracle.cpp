@@ -30,6 +30,7 @@
 // Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fopenmp).
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -1551,4 +1552,56 @@ int oracle_object_intersects(const grt_scene_desc* d, int object, const double* 
   return hit ? 1 : 0;
 }
 
+// ---- output stage (color.rs:193-298), as Raytracer::render_section calls it for
+// non-HDR files (raytracer.rs:481-487): xyz_to_linear_srgb_buffer, then
+// linear_srgb_to_srgb_buffer(.., exposure, tone_mapping).
+static double out_compand_srgb(double linear) {  // color.rs:193-202
+  double sign = linear < 0.0 ? -1.0 : 1.0;
+  double a = std::fabs(linear);
+  double encoded = a <= 0.003'130'8 ? 12.92 * a : 1.055 * std::pow(a, 1.0 / 2.4) - 0.055;
+  double v = sign * encoded;
+  return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);  // f64::clamp
+}
+static uint8_t out_round_u8(double v) {  // (v * 255.0).round() as u8
+  double r = std::round(v * 255.0);
+  if (std::isnan(r) || r <= 0.0) return 0;
+  return r >= 255.0 ? 255 : (uint8_t)r;
+}
+void oracle_xyz_to_srgb8(const double* xyza, uint64_t n, int tone, double exposure, uint8_t* rgb) {
+  static const double M[3][3] = {{3.240'625'5, -1.537'208'0, -0.498'628'6},
+                                 {-0.968'930'7, 1.875'756'1, 0.041'517'5},
+                                 {0.055'710'1, -0.204'021'1, 1.056'995'9}};
+  std::vector<std::array<double, 3>> lin(n);
+  for (uint64_t i = 0; i < n; ++i)  // m * v: nalgebra gemv, column by column
+    for (int r = 0; r < 3; ++r) {
+      double acc = M[r][0] * xyza[4 * i];
+      acc = M[r][1] * xyza[4 * i + 1] + acc;
+      acc = M[r][2] * xyza[4 * i + 2] + acc;
+      lin[i][r] = acc;
+    }
+  double scale = 1.0;
+  if (tone == 1) {  // GlobalLinear: fold(0.0, f64::max) per channel
+    double mx[3] = {0.0, 0.0, 0.0};
+    for (int k = 0; k < 3; ++k)
+      for (uint64_t i = 0; i < n; ++i) mx[k] = std::fmax(mx[k], lin[i][k] * exposure);
+    double max_component = std::fmax(std::fmax(mx[0], mx[1]), mx[2]);
+    scale = max_component > 0.0 ? 1.0 / max_component : 1.0;
+  }
+  for (uint64_t i = 0; i < n; ++i) {
+    double c[3] = {lin[i][0] * exposure, lin[i][1] * exposure, lin[i][2] * exposure};
+    if (tone == 0) {  // Reinhard on luminance
+      double l_in = 0.2126 * c[0] + 0.7152 * c[1] + 0.0722 * c[2];
+      if (l_in > 0.0) {
+        double l_out = l_in / (1.0 + l_in);
+        double f = l_out / l_in;
+        for (int k = 0; k < 3; ++k) c[k] = c[k] * f;
+      }
+    } else {
+      for (int k = 0; k < 3; ++k) c[k] = scale * c[k];
+    }
+    for (int k = 0; k < 3; ++k) rgb[3 * i + k] = out_round_u8(out_compand_srgb(std::fmax(c[k], 0.0)));
+  }
+}
+
 }  // extern "C"
+

@@ -52,6 +52,7 @@ def lib():
         L.oracle_texture_color.argtypes = [vp, C.c_int, _d, _d, _d, _d, _pd]
         L.oracle_killing_coefficients.argtypes = [_d, _d, _d, _pd, _pd]
         L.oracle_object_intersects.argtypes = [vp, C.c_int, _pd, _pd, _pd, _pd]
+        L.oracle_xyz_to_srgb8.argtypes = [_pd, C.c_uint64, C.c_int, _d, _u8p]
         _lib = L
     return _lib
 
@@ -172,3 +173,11 @@ def object_intersects(desc, obj, a, b):
     pt, t = np.zeros(4), C.c_double()
     hit = lib().oracle_object_intersects(_addr(desc), obj, _dp(pa), _dp(pb), _dp(pt), C.byref(t))
     return bool(hit), pt, t.value
+
+
+def xyz_to_srgb8(xyza, tone: int, exposure: float = 1.0):
+    """color.rs:204-298 output stage: (n,4) f64 XYZA -> (n,3) u8 sRGB."""
+    x = np.ascontiguousarray(xyza, np.float64).reshape(-1, 4)
+    out = np.zeros((x.shape[0], 3), np.uint8)
+    lib().oracle_xyz_to_srgb8(_dp(x), x.shape[0], tone, exposure, out.ctypes.data_as(_u8p))
+    return out
