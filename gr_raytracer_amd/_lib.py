@@ -123,6 +123,14 @@ def lib() -> C.CDLL:
             f"{LIB_PATH} not found: the HIP extension is not built "
             "(run `python -c 'import __graft_entry__; __graft_entry__.build()'` or "
             "`make -C gr_raytracer_amd/csrc`). There is no CPU fallback.")
+    # libgrt.so and torch's ROCm build both need libamdhip64.so.7; the first one loaded
+    # serves the whole process.  torch refuses a HIP runtime other than its own ("No HIP
+    # GPUs are available"), while libgrt runs on either, so torch (plumbing for device
+    # buffers, streams and torch.distributed) is loaded first when it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     vp, u32, u64, i32, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32, C.c_int64
     sigs = {

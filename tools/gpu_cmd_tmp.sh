@@ -1,5 +1,3 @@
 set -o pipefail
-mkdir -p gpurun_out/r01i
-timeout -k 10 900 python3 tools/time_variants.py base div lds_div > gpurun_out/r01i/variants.log 2>&1; rc=$?
-cat gpurun_out/r01i/variants.log
-exit $rc
+cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python3 -m pytest tests/test_output_stage.py -m gpu -q -rA -p no:cacheprovider > gpurun_out/out_stage.log 2>&1
