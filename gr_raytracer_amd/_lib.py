@@ -140,6 +140,7 @@ def lib() -> C.CDLL:
         "grt_default_adaptive_config": (None, [C.POINTER(AdaptiveConfig)]),
         "grt_host_scene_load": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(GlobalOpts), C.POINTER(vp)]),
         "grt_host_scene_desc": (C.POINTER(SceneDesc), [vp]),
+        "grt_host_geometry_load": (C.c_int, [C.c_char_p, C.POINTER(GlobalOpts), C.POINTER(vp)]),
         "grt_host_scene_adaptive": (None, [vp, C.POINTER(AdaptiveConfig)]),
         "grt_host_scene_destroy": (C.c_int, [vp]),
         "grt_camera_build": (C.c_int, [i32, _d, _d, _pd, _pd, _d, i64, i64, _d, _d, _d, C.POINTER(CameraDesc)]),
@@ -172,8 +173,20 @@ def lib() -> C.CDLL:
         "grt_linear_max_async": (C.c_int, [C.c_int, vp, vp, u64, _d, vp]),
         "grt_tonemap_async": (C.c_int, [C.c_int, vp, vp, u64, i32, _d, vp, vp]),
         "grt_xyz_to_srgb8_device": (C.c_int, [C.c_int, _pd, C.c_size_t, i32, _d, C.POINTER(C.c_uint8)]),
+        "grt_trace_pixels": (C.c_int, [vp, C.c_int, u64, _pd, _pd, u64, _pd, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
+        "grt_trace_rays": (C.c_int, [vp, C.c_int, u64, _pd, _pd, u64, _pd, C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
+        "grt_ray_at": (C.c_int, [i32, _d, _d, _pd, _pd, _pd, _pd]),
+        "grt_write_trajectory_csv": (C.c_int, [C.c_char_p, i32, _d, _pd, u64]),
+        "grt_format_f64": (C.c_size_t, [_d, C.c_char_p, C.c_size_t]),
     }
+    # GRT_LIB_ALLOW_MISSING=1 (tools/time_variants.py only) binds an older experimental
+    # build that lacks newer entry points; by default a missing symbol is an error.
+    allow_missing = os.environ.get("GRT_LIB_ALLOW_MISSING") == "1"
     for name, (res, args) in sigs.items():
+        if allow_missing and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -183,13 +196,14 @@ def lib() -> C.CDLL:
 
 EXPORTED_SYMBOLS = [
     "grt_last_error", "grt_device_count", "grt_default_global_opts", "grt_default_adaptive_config",
-    "grt_host_scene_load", "grt_host_scene_desc", "grt_host_scene_adaptive", "grt_host_scene_destroy",
+    "grt_host_scene_load", "grt_host_geometry_load", "grt_host_scene_desc", "grt_host_scene_adaptive", "grt_host_scene_destroy",
     "grt_camera_build", "grt_stationary_velocity", "grt_zamo_velocity", "grt_cartesian_to_spherical",
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
     "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_xyz_to_srgb8", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
     "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config",
     "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
-    "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device",
+    "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",
+    "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64",
 ]
 
 

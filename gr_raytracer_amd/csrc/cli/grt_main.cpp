@@ -7,7 +7,10 @@
 //       [--sampling-mask-color r,g,b] --config-file scene.toml
 //       render [--filename out.png|out.hdr] [--from-row N] [--from-col N]
 //              [--to-row N] [--to-col N]
+//     | render-ray -r ROW -c COL [--filename rendered-ray.csv]
+//     | render-ray-at -p x,y,z -d x,y,z [--filename rendered-ray-at.csv]
 //
+// Global options go before the subcommand, subcommand options after it (clap).
 // Extra (not in the reference): --device N selects the GPU, --resource-root DIR
 // resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer.
 #include <chrono>
@@ -26,7 +29,11 @@ bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint3
 }
 
 static int usage(const char* msg) {
-  std::fprintf(stderr, "error: %s\nusage: grt [global options] --config-file FILE render [--filename F]\n", msg);
+  std::fprintf(stderr,
+               "error: %s\nusage: grt [global options] --config-file FILE render [--filename F]\n"
+               "       grt [global options] --config-file FILE render-ray -r ROW -c COL [--filename F]\n"
+               "       grt [global options] --config-file FILE render-ray-at -p X,Y,Z -d X,Y,Z [--filename F]\n",
+               msg);
   return 2;
 }
 
@@ -46,12 +53,59 @@ static bool split_csv(const std::string& s, std::vector<double>& out) {
   return true;
 }
 
+static const char* stop_name(int s) {  // integrator.rs StopReason, as logged by the reference
+  switch (s) {
+    case GRT_STOP_HORIZON: return "Some(HorizonReached)";
+    case GRT_STOP_CELESTIAL: return "Some(CelestialSphereReached)";
+    case GRT_STOP_NAN: return "Some(CoordinateIsNan)";
+    case GRT_STOP_CLOSED_ORBIT: return "Some(ClosedOrbitDetected)";
+    default: return "None";
+  }
+}
+
+// render-ray / render-ray-at: integrate one ray on the GPU and save its trajectory
+// (main.rs:117-171).  The file is created before integrating, as the reference does.
+static int trace_and_save(grt_scene* scene, int device, const grt_scene_desc* d, bool camera, const double* a,
+                          const double* b, const std::string& filename) {
+  FILE* f = std::fopen(filename.c_str(), "wb");
+  if (!f) {
+    std::fprintf(stderr, "Error: cannot create %s\n", filename.c_str());
+    return 1;
+  }
+  std::fclose(f);
+  const uint64_t cap = d->max_steps > 0 ? d->max_steps : 1;  // steps 0 .. max_steps-1
+  std::vector<double> steps(cap * 9);
+  uint64_t n = 0;
+  uint8_t stop = 0, status = 0;
+  int rc = camera ? grt_trace_pixels(scene, device, 1, a, b, cap, steps.data(), &n, &stop, &status)
+                  : grt_trace_rays(scene, device, 1, a, b, cap, steps.data(), &n, &stop, &status);
+  if (rc) {
+    std::fprintf(stderr, "Error: %s\n", grt_last_error());
+    return 1;
+  }
+  if (status != GRT_OK) {
+    std::fprintf(stderr, "Error: %s\n", status == GRT_ERR_MAX_STEPS_REACHED ? "Max steps reached" : "integration failed");
+    return 1;
+  }
+  std::fprintf(stderr, "Stop reason: %s\n", stop_name(stop));
+  if (grt_write_trajectory_csv(filename.c_str(), d->geometry, d->a, steps.data(), n < cap ? n : cap)) {
+    std::fprintf(stderr, "Error: %s\n", grt_last_error());
+    return 1;
+  }
+  std::fprintf(stderr, "Saved integrated ray to %s\n", filename.c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   auto t_start = std::chrono::steady_clock::now();
   grt_global_opts opts;
   grt_default_global_opts(&opts);
-  std::string config_file, action, filename = "render.png", resource_root, raw_out;
+  std::string config_file, action, filename, resource_root, raw_out;
   long from_row = -1, from_col = -1, to_row = -1, to_col = -1;
+  long long ray_row = 0, ray_col = 0;
+  bool have_row = false, have_col = false;
+  std::vector<double> ray_position, ray_direction;
+  bool have_position = false, have_direction = false;
   int device = 0;
   std::vector<std::string> args(argv + 1, argv + argc);
   for (size_t i = 0; i < args.size(); ++i) {
@@ -73,12 +127,36 @@ int main(int argc, char** argv) {
       return true;
     };
     std::string v;
-    if (a == "render") { action = a; continue; }
-    if (a == "render-ray" || a == "render-ray-at" || a == "blackbody" || a == "blackbody-spectrum")
+    if (action.empty() && (a == "render" || a == "render-ray" || a == "render-ray-at")) {
+      action = a;
+      continue;
+    }
+    if (action.empty() && (a == "blackbody" || a == "blackbody-spectrum"))
       return usage(("subcommand '" + a + "' is outside this build's hot-path scope").c_str());
-    if (a == "--show-sampling-mask") { opts.show_sampling_mask = 1; continue; }
+    if (action.empty() && a == "--show-sampling-mask") { opts.show_sampling_mask = 1; continue; }
     if (!next(v)) return usage(("missing value for " + a).c_str());
     std::vector<double> nums;
+    // extras accepted anywhere
+    if (a == "--device") { device = std::atoi(v.c_str()); continue; }
+    if (a == "--resource-root") { resource_root = v; continue; }
+    if (a == "--raw-out") { raw_out = v; continue; }
+    if (!action.empty()) {  // subcommand options
+      if (a == "--filename") filename = v;
+      else if (action == "render" && a == "--from-row") from_row = std::atol(v.c_str());
+      else if (action == "render" && a == "--from-col") from_col = std::atol(v.c_str());
+      else if (action == "render" && a == "--to-row") to_row = std::atol(v.c_str());
+      else if (action == "render" && a == "--to-col") to_col = std::atol(v.c_str());
+      else if (action == "render-ray" && (a == "-r" || a == "--row")) { ray_row = std::atoll(v.c_str()); have_row = true; }
+      else if (action == "render-ray" && (a == "-c" || a == "--col")) { ray_col = std::atoll(v.c_str()); have_col = true; }
+      else if (action == "render-ray-at" && (a == "-p" || a == "--position")) {
+        if (!split_csv(v, ray_position)) return usage("invalid position");
+        have_position = true;
+      } else if (action == "render-ray-at" && (a == "-d" || a == "--direction")) {
+        if (!split_csv(v, ray_direction)) return usage("invalid direction");
+        have_direction = true;
+      } else return usage(("unknown argument " + a + " for " + action).c_str());
+      continue;
+    }
     if (a == "--width") opts.width = std::atoll(v.c_str());
     else if (a == "--height") opts.height = std::atoll(v.c_str());
     else if (a == "--step-size") opts.step_size = std::atof(v.c_str());
@@ -92,8 +170,8 @@ int main(int argc, char** argv) {
       if (!split_csv(v, nums) || nums.size() != 3) return usage("Camera position must be a vector of length 3");
       for (int k = 0; k < 3; ++k) opts.camera_position[k] = nums[k];
     } else if (a == "--tone-mapping") {
-      if (v == "reinhard") opts.tone_mapping = 0;
-      else if (v == "global-linear") opts.tone_mapping = 1;
+      if (v == "reinhard") opts.tone_mapping = GRT_TONE_REINHARD;
+      else if (v == "global-linear") opts.tone_mapping = GRT_TONE_GLOBAL_LINEAR;
       else return usage("tone mapping must be reinhard or global-linear");
     } else if (a == "--sampling-mask-color") {
       if (!split_csv(v, nums) || nums.size() != 3) return usage("invalid RGB color; expected R,G,B");
@@ -102,21 +180,21 @@ int main(int argc, char** argv) {
         opts.sampling_mask_color[k] = (uint8_t)nums[k];
       }
     } else if (a == "-c" || a == "--config-file") config_file = v;
-    else if (a == "--filename") filename = v;
-    else if (a == "--from-row") from_row = std::atol(v.c_str());
-    else if (a == "--from-col") from_col = std::atol(v.c_str());
-    else if (a == "--to-row") to_row = std::atol(v.c_str());
-    else if (a == "--to-col") to_col = std::atol(v.c_str());
-    else if (a == "--device") device = std::atoi(v.c_str());
-    else if (a == "--resource-root") resource_root = v;
-    else if (a == "--raw-out") raw_out = v;
     else return usage(("unknown argument " + a).c_str());
   }
-  if (action != "render") return usage("missing subcommand (render)");
+  if (action.empty()) return usage("missing subcommand (render, render-ray, render-ray-at)");
+  if (action == "render-ray" && !(have_row && have_col)) return usage("render-ray needs --row and --col");
+  if (action == "render-ray-at" && !(have_position && have_direction))
+    return usage("render-ray-at needs --position and --direction");
+  if (filename.empty())
+    filename = action == "render" ? "render.png" : (action == "render-ray" ? "rendered-ray.csv" : "rendered-ray-at.csv");
   if (config_file.empty()) return usage("Config file is required for this action");
 
   grt_host_scene* hs = nullptr;
-  if (grt_host_scene_load(config_file.c_str(), resource_root.empty() ? nullptr : resource_root.c_str(), &opts, &hs)) {
+  if (action == "render-ray-at" ? grt_host_geometry_load(config_file.c_str(), &opts, &hs)
+                                : grt_host_scene_load(config_file.c_str(),
+                                                      resource_root.empty() ? nullptr : resource_root.c_str(), &opts,
+                                                      &hs)) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
@@ -126,6 +204,32 @@ int main(int argc, char** argv) {
   if (grt_scene_create(grt_host_scene_desc(hs), &scene)) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
+  }
+  const grt_scene_desc* d = grt_host_scene_desc(hs);
+  if (action != "render") {
+    int rc;
+    if (action == "render-ray") {  // Raytracer::integrate_ray_at_point (raytracer.rs:499-507)
+      const double row = (double)ray_row, col = (double)ray_col;
+      rc = trace_and_save(scene, device, d, true, &row, &col, filename);
+    } else {
+      if (ray_position.size() != 3) {
+        std::fprintf(stderr, "Error: Position must be a vector of length 3, got %zu values\n", ray_position.size());
+        return 1;
+      }
+      if (ray_direction.size() != 3) {
+        std::fprintf(stderr, "Error: Direction must be a vector of length 3, got %zu values\n", ray_direction.size());
+        return 1;
+      }
+      double pos[4], mom[4];
+      if (grt_ray_at(d->geometry, d->radius, d->a, ray_position.data(), ray_direction.data(), pos, mom)) {
+        std::fprintf(stderr, "Error: %s\n", grt_last_error());
+        return 1;
+      }
+      rc = trace_and_save(scene, device, d, false, pos, mom, filename);
+    }
+    grt_scene_destroy(scene);
+    grt_host_scene_destroy(hs);
+    return rc;
   }
   uint32_t r0 = from_row < 0 ? 0 : (uint32_t)from_row, c0 = from_col < 0 ? 0 : (uint32_t)from_col;
   uint32_t r1 = to_row < 0 ? (uint32_t)opts.height : (uint32_t)to_row;

@@ -516,6 +516,63 @@ int grt_render_pixels(grt_scene* s, int device, uint32_t row0, uint32_t col0, ui
   return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
 }
 
+// Shared body of grt_trace_pixels / grt_trace_rays: a, b are (row, col) or (pos, mom).
+static int trace_common(grt_scene* s, int device, uint64_t n, bool camera, const double* a, const double* b,
+                        uint64_t capacity, double* steps_out, uint64_t* n_steps, uint8_t* stop_out,
+                        uint8_t* status_out) {
+  if (!s || !n_steps || !stop_out || !status_out || (n && (!a || !b)) || (capacity && !steps_out))
+    return fail(-EINVAL, "null argument");
+  if (n == 0) return 0;
+  if (capacity > (1ull << 40) / 72 / n) return fail(-EINVAL, "trajectory buffer too large");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  const uint64_t in_bytes = n * 8 * (camera ? 1 : 4);
+  DevBuf b_a, b_b, b_steps, b_n, b_stop, b_status;
+  if ((rc = b_a.alloc(in_bytes)) || (rc = b_b.alloc(in_bytes)) || (rc = b_steps.alloc(n * capacity * 72)) ||
+      (rc = b_n.alloc(n * 8)) || (rc = b_stop.alloc(n)) || (rc = b_status.alloc(n)))
+    return rc;
+  HIP_TRY(hipMemcpy(b_a.p, a, in_bytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(b_b.p, b, in_bytes, hipMemcpyHostToDevice));
+  grt::TrajectoryList tl;
+  std::memset(&tl, 0, sizeof(tl));
+  tl.n = n;
+  if (camera) {
+    tl.row = (const double*)b_a.p;
+    tl.col = (const double*)b_b.p;
+  } else {
+    tl.pos = (const double*)b_a.p;
+    tl.mom = (const double*)b_b.p;
+  }
+  tl.cap = capacity;
+  tl.steps = (double*)b_steps.p;
+  tl.n_steps = (uint64_t*)b_n.p;
+  tl.stop = (uint8_t*)b_stop.p;
+  tl.status = (uint8_t*)b_status.p;
+  HIP_TRY(grt::launch_trajectories(s->desc.geometry, dc->d_scene, tl, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  if (capacity) HIP_TRY(hipMemcpy(steps_out, b_steps.p, n * capacity * 72, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(n_steps, b_n.p, n * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(stop_out, b_stop.p, n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int grt_trace_pixels(grt_scene* s, int device, uint64_t n, const double* rows, const double* cols,
+                     uint64_t capacity, double* steps_out, uint64_t* n_steps, uint8_t* stop_out,
+                     uint8_t* status_out) {
+  return trace_common(s, device, n, true, rows, cols, capacity, steps_out, n_steps, stop_out, status_out);
+}
+
+int grt_trace_rays(grt_scene* s, int device, uint64_t n, const double* positions, const double* momenta,
+                   uint64_t capacity, double* steps_out, uint64_t* n_steps, uint8_t* stop_out,
+                   uint8_t* status_out) {
+  return trace_common(s, device, n, false, positions, momenta, capacity, steps_out, n_steps, stop_out,
+                      status_out);
+}
+
 int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
                        uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza,
                        double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats) {

@@ -765,21 +765,18 @@ GDEV void camera_momentum(const DevCamera& c, double row, double column, double*
   }
 }
 
-// Create the ray state (integrator.rs:82-99 + geometry-specific create_initial_state);
-// writes the per-ray constants (observer energy, KerrBL E/L_z/Q) to the workspace.
+// Initial ODE state of a ray at native-chart position `pos` with contravariant momentum
+// `p` (integrator.rs:82-99 + the geometry's get_geodesic_solver / create_initial_state);
+// st, ct = sin / cos of pos[2] (KerrBL only).  Fills the KerrBL constants E, L_z, Q.
 template <int G>
-GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayConst& rc) {
-  const DevCamera& cam = S.cam;
-  double p[4];
-  camera_momentum(cam, row, col, p);
-  rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);  // redshift.rs:40-43
+GDEV void init_state(const DevScene& S, const double* pos, double st, double ct, const double* p, double* y,
+                     RayConst& rc) {
   rc.e = 0.0;
   rc.lz = 0.0;
   rc.q = 0.0;
   if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:505-577, :176-223 (BL ray)
     double a = S.a, radius = S.radius;
-    double r = cam.pos[1];
-    double st = cam.sin_theta, ct = cam.cos_theta;
+    double r = pos[1];
     double g[4][4];
     metric_bl(radius, a, r, st, ct, g);
     double pc[4];
@@ -797,31 +794,42 @@ GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayCons
     double le = l_z - a * e;
     double r_pot = p_r * p_r - del * (le * le + q);
     double th_pot = q + a * a * e * e * ct * ct - l_z * l_z * ct * ct / (st * st);
-    y[0] = cam.pos[0];
+    y[0] = pos[0];
     y[1] = r;
-    y[2] = cam.pos[2];
-    y[3] = cam.pos[3];
+    y[2] = pos[2];
+    y[3] = pos[3];
     y[4] = sign_r * sqrt(fmax(r_pot, 0.0));
     y[5] = sign_theta * sqrt(fmax(th_pot, 0.0));
     y[6] = 0.0;
     y[7] = 0.0;
   } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:243-260
     double g[4][4];
-    ks_metric(S.radius, S.a, cam.pos[1], cam.pos[2], cam.pos[3], g);
+    ks_metric(S.radius, S.a, pos[1], pos[2], pos[3], g);
     double pc[4];
     mat_vec(g, p, pc);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      y[k] = cam.pos[k];
+      y[k] = pos[k];
       y[4 + k] = pc[k];
     }
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      y[k] = cam.pos[k];
+      y[k] = pos[k];
       y[4 + k] = p[k];
     }
   }
+}
+
+// Create a camera ray's state (camera.rs:234-254 + init_state); also the observer
+// energy the redshift needs (redshift.rs:40-43).
+template <int G>
+GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayConst& rc) {
+  const DevCamera& cam = S.cam;
+  double p[4];
+  camera_momentum(cam, row, col, p);
+  init_state<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, p, y, rc);
+  rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
 }
 
 // integrator.rs:203-268
@@ -896,6 +904,33 @@ GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
     }
     return true;
   }
+}
+
+// The step-size controller of rkf45 (runge_kutta.rs:148-178) after one attempt with
+// error norm `err` at step h_cur.  Accepted: h_next is the next step's h.  Rejected:
+// h_cur is the retry's step (STEP_RETRY), or the 100th retry failed (STEP_FAILED,
+// Err(MaxStepsReached)).
+enum { STEP_ACCEPTED = 0, STEP_RETRY = 1, STEP_FAILED = 2 };
+GDEV int step_control(const DevScene& S, double err, double& h_cur, int& retries, double& h_next) {
+  // h_prop = err > 0 ? BETA*h*(eps/err)^(1/5) : 4h, then min(., 4h).  For eps/err >= 1800,
+  // BETA*1800^(1/5) = 4.0308 > 4, so the min is 4h whatever pow's last ulp: pow is
+  // skipped there (the far-field steps), which leaves every result bit-identical.
+  double h_prop = h_cur * H_GROWTH;
+  if (err > 0.0) {
+    const double ratio = S.epsilon / err;
+    if (ratio < POW_SATURATED) h_prop = BETA * h_cur * rpow(ratio, INV_ORDER);
+  }
+  h_prop = rclamp(fmin(h_prop, h_cur * H_GROWTH), H_MIN, H_MAX);
+  if (err > S.epsilon) {
+    if (h_cur <= H_MIN) {
+      h_next = h_cur;
+      return STEP_ACCEPTED;
+    }
+    h_cur = rclamp(h_prop / 2.0, H_MIN, H_MAX);
+    return (++retries >= MAX_RETRY) ? STEP_FAILED : STEP_RETRY;
+  }
+  h_next = (err / S.epsilon < SMALL_ERR) ? rclamp(h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
+  return STEP_ACCEPTED;
 }
 
 // End of a ray: its final state goes to the workspace for the shade kernel.
@@ -1011,29 +1046,14 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     double yn[8];
     double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
     n_att++;
-    // h_prop = err > 0 ? BETA*h*(eps/err)^(1/5) : 4h, then min(., 4h).  For eps/err >= 1800,
-    // BETA*1800^(1/5) = 4.0308 > 4, so the min is 4h whatever pow's last ulp: pow is
-    // skipped there (the far-field steps), which leaves every result bit-identical.
-    double h_prop = h_cur * H_GROWTH;
-    if (err > 0.0) {
-      const double ratio = S.epsilon / err;
-      if (ratio < POW_SATURATED) h_prop = BETA * h_cur * rpow(ratio, INV_ORDER);
-    }
-    h_prop = rclamp(fmin(h_prop, h_cur * H_GROWTH), H_MIN, H_MAX);
     double h_next;
-    if (err > S.epsilon) {
-      if (h_cur <= H_MIN) {
-        h_next = h_cur;
-      } else {
-        h_cur = rclamp(h_prop / 2.0, H_MIN, H_MAX);
-        if (++retries >= MAX_RETRY) {  // Err(MaxStepsReached)
-          store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
-          active = false;
-        }
-        continue;
+    const int ctl = step_control(S, err, h_cur, retries, h_next);
+    if (ctl != STEP_ACCEPTED) {
+      if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
+        store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
+        active = false;
       }
-    } else {
-      h_next = (err / S.epsilon < SMALL_ERR) ? rclamp(h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
+      continue;
     }
 
     // ---------------- accepted step i (integrator.rs:100-162) --------------------
@@ -1107,6 +1127,89 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     atomicAdd(stats + 1, (unsigned long long)n_att);
     atomicAdd(stats + 2, (unsigned long long)n_rays);
   }
+}
+
+// ======================================================= trajectory kernel =======
+// Integrator::integrate with the whole Vec<Step> kept (integrator.rs:78-174), the path
+// of `render-ray` / `render-ray-at` (main.rs:117-171, ray.rs:35-54).  One lane per ray;
+// step 0 is the initial state.  Each record is (t, x^0..x^3, p^0..p^3): the affine
+// parameter, the native-chart position and momentum_from_state.  Steps beyond the
+// caller's capacity are counted but not stored.
+template <int G>
+__global__ void __launch_bounds__(64) trajectory_kernel(const DevScene* __restrict__ Sp, TrajectoryList tl) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before the early return
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= tl.n) return;
+  double y[8];
+  RayConst rc;
+  if (tl.row) {
+    init_ray<G>(S, tl.row[r], tl.col[r], y, rc);
+  } else {
+    double st = 0.0, ct = 0.0;
+    if constexpr (G == GRT_GEOM_KERR_BL) rsincos(tl.pos[4 * r + 2], &st, &ct);
+    init_state<G>(S, tl.pos + 4 * r, st, ct, tl.mom + 4 * r, y, rc);
+  }
+  uint64_t count = 0;
+  auto record = [&](double t) {
+    if (count < tl.cap) {
+      double* o = tl.steps + (r * tl.cap + count) * 9;
+      o[0] = t;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[1 + k] = y[k];
+      momentum<G>(S, rc, y, o + 5);
+    }
+    count++;
+  };
+  record(0.0);
+  int stop = GRT_STOP_NONE, status = GRT_OK;
+  double t = 0.0, h = S.step_size;
+  for (uint64_t i = 1; i < S.max_steps; ++i) {
+    double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
+    int retries = 0, ctl;
+    do {
+      const double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
+      ctl = step_control(S, err, h_cur, retries, h_next);
+    } while (ctl == STEP_RETRY);
+    if (ctl == STEP_FAILED) {
+      status = GRT_ERR_MAX_STEPS_REACHED;
+      break;
+    }
+    t += h_cur;
+    h = h_next;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = yn[k];
+    record(t);
+    double c[3];
+    bool c_valid = false;
+    stop = should_stop<G>(S, y, c, c_valid, i);
+    if (stop != GRT_STOP_NONE) break;
+  }
+  tl.n_steps[r] = count;
+  tl.stop[r] = (uint8_t)stop;
+  tl.status[r] = (uint8_t)status;
+}
+
+hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream) {
+  if (tl.n == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((tl.n + 63) / 64);
+  switch (geometry) {
+    case GRT_GEOM_EUCLIDEAN:
+      hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_EUCLIDEAN>, dim3(blocks), dim3(64), 0, stream, d_scene, tl);
+      break;
+    case GRT_GEOM_SCHWARZSCHILD:
+      hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_SCHWARZSCHILD>, dim3(blocks), dim3(64), 0, stream, d_scene, tl);
+      break;
+    case GRT_GEOM_KERR:
+      hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_KERR>, dim3(blocks), dim3(64), 0, stream, d_scene, tl);
+      break;
+    case GRT_GEOM_KERR_BL:
+      hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, tl);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // ============================================================ shade kernel =======

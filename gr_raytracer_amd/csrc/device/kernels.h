@@ -11,6 +11,22 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
                         int blocks, int threads, hipStream_t stream);
 
+// Whole trajectories (render-ray / render-ray-at): camera pixels (row, col) or explicit
+// native-chart (position, momentum) pairs; record layout in trajectory_kernel.
+struct TrajectoryList {
+  uint64_t n;
+  const double* row;  // camera mode: pixel coordinates (offsets allowed), both non-null
+  const double* col;
+  const double* pos;  // explicit mode: n x 4 each
+  const double* mom;
+  uint64_t cap;       // records stored per ray
+  double* steps;      // n x cap x 9
+  uint64_t* n_steps;  // steps produced per ray (step 0 included), even beyond cap
+  uint8_t* stop;
+  uint8_t* status;
+};
+hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
+
 // Adaptive supersampling helpers (raytracer.rs:91-159, :320-458).
 struct AdaptiveParams {
   uint32_t w, h;  // section size

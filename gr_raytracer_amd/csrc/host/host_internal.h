@@ -31,6 +31,9 @@ void linear_max(const double* xyza, size_t n, double exposure, double* max3);
 int tonemap(const double* xyza, size_t n, int tone, double exposure, const double* max3, uint8_t* rgb);
 int stationary(int geometry, double radius, double a, const double position[4], double out[4]);
 int zamo(int geometry, double radius, double a, const double position[4], double out[4]);
+int ray_at(int geometry, double radius, double a, const double position[3], const double direction[3],
+           double pos_out[4], double mom_out[4], std::string& err);
+std::string rust_display_f64(double v);
 
 // ---- minimal TOML (the subset the reference's scene files use) ----
 struct TomlValue;

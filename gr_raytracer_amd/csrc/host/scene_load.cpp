@@ -217,23 +217,17 @@ void grt_default_adaptive_config(grt_adaptive_config* c) {  // configuration.rs:
   c->exclude_background_contrast = 1;
 }
 
-int grt_host_scene_load(const char* toml_path, const char* resource_root, const grt_global_opts* opts,
-                        grt_host_scene** out) {
-  if (!toml_path || !opts || !out) return fail("null argument");
+// Read the TOML file, then geometry_type (configuration.rs:111-158) and the integration
+// configuration from GlobalOpts into a fresh descriptor.
+static int load_geometry(const char* toml_path, const grt_global_opts* opts, TomlTable& root, grt_scene_desc& d) {
   std::ifstream f(toml_path);
   if (!f) return fail(std::string("Config file not found: ") + toml_path);
   std::stringstream ss;
   ss << f.rdbuf();
-  TomlTable root;
   std::string err;
   if (!toml_parse(ss.str(), root, err)) return fail("TOML error: " + err);
-
-  std::unique_ptr<grt_host_scene> hs(new grt_host_scene());
-  grt_scene_desc& d = hs->desc;
   std::memset(&d, 0, sizeof(d));
   d.abi_version = GRT_ABI_VERSION;
-
-  // geometry_type (configuration.rs:111-158)
   std::string gname;
   const TomlTable* gb;
   if (!variant(get(root, "geometry_type"), gname, &gb)) return fail("missing or invalid `geometry_type`");
@@ -250,6 +244,41 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
   } else {
     return fail("geometry `" + gname + "` is out of scope (Euclidean, Schwarzschild, Kerr, KerrBL supported)");
   }
+  d.max_steps = opts->max_steps;
+  d.max_radius = opts->max_radius;
+  d.step_size = opts->step_size;
+  d.epsilon = opts->epsilon;
+  for (int i = 0; i < 256; ++i) d.srgb_to_linear[i] = inv_compand_srgb((double)i / 255.0);
+  d.object_hit_opacity_threshold = 0.5;
+  return 0;
+}
+
+int grt_host_geometry_load(const char* toml_path, const grt_global_opts* opts, grt_host_scene** out) {
+  if (!toml_path || !opts || !out) return fail("null argument");
+  std::unique_ptr<grt_host_scene> hs(new grt_host_scene());
+  TomlTable root;
+  int rc = load_geometry(toml_path, opts, root, hs->desc);
+  if (rc) return rc;
+  grt_default_adaptive_config(&hs->adaptive);
+  grt_scene_desc& d = hs->desc;
+  // no camera, no objects: a 1x1 placeholder frame and a constant black sky
+  d.camera.rows = d.camera.cols = 1;
+  d.celestial.kind = GRT_TEX_CHECKER;
+  d.celestial.checker_width = d.celestial.checker_height = 1.0;
+  d.celestial.c1[3] = d.celestial.c2[3] = 1.0;
+  *out = hs.release();
+  return 0;
+}
+
+int grt_host_scene_load(const char* toml_path, const char* resource_root, const grt_global_opts* opts,
+                        grt_host_scene** out) {
+  if (!toml_path || !opts || !out) return fail("null argument");
+  std::unique_ptr<grt_host_scene> hs(new grt_host_scene());
+  grt_scene_desc& d = hs->desc;
+  TomlTable root;
+  std::string err;
+  int rc0 = load_geometry(toml_path, opts, root, d);
+  if (rc0) return rc0;
 
   // adaptive_sampling (configuration.rs:21-94), serde(default) per field
   grt_adaptive_config& ac = hs->adaptive;
@@ -281,13 +310,6 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
   if (ac.has_minimum_luminance && (!std::isfinite(ac.minimum_luminance) || ac.minimum_luminance < 0.0))
     return fail("adaptive_sampling.minimum_luminance must be finite and non-negative");
   d.object_hit_opacity_threshold = ac.object_hit_opacity_threshold;
-
-  // integration configuration from GlobalOpts
-  d.max_steps = opts->max_steps;
-  d.max_radius = opts->max_radius;
-  d.step_size = opts->step_size;
-  d.epsilon = opts->epsilon;
-  for (int i = 0; i < 256; ++i) d.srgb_to_linear[i] = inv_compand_srgb((double)i / 255.0);
 
   // camera position in the geometry's native chart (cli/<geometry>.rs)
   double cart[4] = {0.0, opts->camera_position[0], opts->camera_position[1], opts->camera_position[2]};

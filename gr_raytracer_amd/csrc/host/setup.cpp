@@ -492,6 +492,66 @@ bool future_directed(int geometry, double radius, double a, const double positio
   double orientation = sig0(g) * inner_product(g, pos, T.t, vv);
   return std::isfinite(vv[0]) && orientation > 0.0;
 }
+// The momentum `render-ray-at` integrates (cli/{euclidean,schwarzschild,kerr,kerr_bl}.rs
+// render_ray_at): a unit spatial direction in the local observer's tetrad at a Cartesian
+// position.  Writes the ray's native-chart position and contravariant momentum.
+int ray_at(int geometry, double radius, double a, const double position[3], const double direction[3],
+           double pos_out[4], double mom_out[4], std::string& err) {
+  Geo g{geometry, radius, a};
+  V4 cart{{0.0, position[0], position[1], position[2]}};
+  const double d1 = direction[0], d2 = direction[1], d3 = direction[2];
+  V4 pos, mom;
+  switch (geometry) {
+    case GRT_GEOM_EUCLIDEAN: {  // cli/euclidean.rs:74-100
+      double spatial_norm = std::sqrt(d1 * d1 + d2 * d2 + d3 * d3);
+      if (!(std::isfinite(spatial_norm) && spatial_norm > 0.0)) {
+        err = "render_ray_at direction must have a non-zero finite spatial part.";
+        return -EINVAL;
+      }
+      pos = cart;
+      mom = V4{{spatial_norm, d1, d2, d3}};
+      break;
+    }
+    case GRT_GEOM_SCHWARZSCHILD: {  // cli/schwarzschild.rs:89-121
+      pos = cart_to_sph_v(cart);
+      double theta = pos[2], phi = pos[3];
+      double r_d = std::sin(theta) * std::cos(phi) * d1 + std::sin(theta) * std::sin(phi) * d2 + std::cos(theta) * d3;
+      double theta_d =
+          std::cos(theta) * std::cos(phi) * d1 + std::cos(theta) * std::sin(phi) * d2 - std::sin(theta) * d3;
+      double phi_d = -std::sin(phi) * d1 + std::cos(phi) * d2;
+      Tetrad T = get_tetrad_at(g, pos);
+      mom = add(add(add(scale(1.0, T.t), scale(phi_d, T.x)), scale(-theta_d, T.y)), scale(-r_d, T.z));
+      break;
+    }
+    default: {  // cli/kerr.rs:77-100 (Cartesian chart), cli/kerr_bl.rs:78-107 (BL chart)
+      if (geometry == GRT_GEOM_KERR) {
+        pos = cart;
+      } else {
+        double out[4];
+        grt_cartesian_to_boyer_lindquist(a, cart.v, out);
+        pos = V4{{out[0], out[1], out[2], out[3]}};
+      }
+      Tetrad T = get_tetrad_at(g, pos);
+      V4 space = add(add(scale(d1, T.x), scale(d2, T.y)), scale(d3, T.z));
+      double norm = std::sqrt(inner_product(g, pos, space, space));
+      V4 m;
+      for (int k = 0; k < 4; ++k)
+        m[k] = ((T.t[k] * 1.0 + T.x[k] * d1 / norm) + T.y[k] * d2 / norm) + T.z[k] * d3 / norm;
+      mom = m;
+      break;
+    }
+  }
+  if (!future_directed(geometry, radius, a, pos.v, mom.v)) {  // cli/shared.rs:79-86
+    err = "render_ray_at momentum is not future-directed";
+    return -EINVAL;
+  }
+  for (int k = 0; k < 4; ++k) {
+    pos_out[k] = pos[k];
+    mom_out[k] = mom[k];
+  }
+  return 0;
+}
+
 double inner(int geometry, double radius, double a, const double position[4], const double v[4], const double w[4]) {
   Geo g{geometry, radius, a};
   V4 pos{{position[0], position[1], position[2], position[3]}};
@@ -833,6 +893,13 @@ void grt_blackbody_xyz(double temperature, double redshift, double out_xyz[3]) {
 }
 void grt_srgb_to_xyza(uint8_t r, uint8_t g, uint8_t b, uint8_t a, double out[4]) {
   grt_host::srgb_to_xyza(r, g, b, a, out);
+}
+int grt_ray_at(int32_t geometry, double radius, double a, const double position[3], const double direction[3],
+               double position_out[4], double momentum_out[4]) {
+  std::string err;
+  int rc = grt_host::ray_at(geometry, radius, a, position, direction, position_out, momentum_out, err);
+  if (rc) grt_host::set_error(err);
+  return rc;
 }
 void grt_linear_max(const double* xyza, size_t n, double exposure, double max3[3]) {
   grt_host::linear_max(xyza, n, exposure, max3);

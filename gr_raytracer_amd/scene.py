@@ -223,6 +223,28 @@ class Scene:
                                            L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st)), "grt_render_section")
         return out, cls, int(nsel.value), _stats_dict(st)
 
+    def _trace(self, fn, a, b, width: int, capacity: int, device: int):
+        a = np.ascontiguousarray(a, np.float64).reshape(-1, width)
+        b = np.ascontiguousarray(b, np.float64).reshape(-1, width)
+        n = a.shape[0]
+        steps = np.zeros((n, capacity, 9), np.float64)
+        n_steps = np.zeros(n, np.uint64)
+        stop, status = np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+        L.check(fn(self._s, device, n, L.dptr(a), L.dptr(b), capacity, L.dptr(steps), L.ptr(n_steps, C.c_uint64),
+                   L.ptr(stop, C.c_uint8), L.ptr(status, C.c_uint8)), "grt_trace")
+        return Trajectories(steps, n_steps.astype(np.int64), stop, status)
+
+    def trace_pixels(self, rows, cols, capacity: Optional[int] = None, device: int = 0) -> "Trajectories":
+        """Whole trajectories of camera rays (Raytracer::integrate_ray_at_point,
+        raytracer.rs:499-507; `render-ray`).  capacity defaults to max_steps records."""
+        cap = int(self.desc.max_steps) if capacity is None else capacity
+        return self._trace(L.lib().grt_trace_pixels, np.atleast_1d(rows), np.atleast_1d(cols), 1, cap, device)
+
+    def trace_rays(self, positions, momenta, capacity: Optional[int] = None, device: int = 0) -> "Trajectories":
+        """Whole trajectories from native-chart positions / contravariant momenta (n x 4)."""
+        cap = int(self.desc.max_steps) if capacity is None else capacity
+        return self._trace(L.lib().grt_trace_rays, positions, momenta, 4, cap, device)
+
     def color_of_ray(self, row: int, col: int, device: int = 0):
         """Colour, class and status of one camera pixel (Scene::color_of_ray)."""
         r = self.render_pixels(row, col, 1, 1, device=device)
@@ -272,6 +294,40 @@ def xyz_to_srgb8(xyza, tone_mapping: int = 0, exposure: float = 1.0, device: Opt
         L.check(L.lib().grt_xyz_to_srgb8_device(device, L.dptr(x), x.shape[0], tone_mapping, exposure,
                                                  L.ptr(out, C.c_uint8)), "grt_xyz_to_srgb8_device")
     return out
+
+
+@dataclass
+class Trajectories:
+    """steps[k, i] = (t, x^0..x^3, p^0..p^3) of ray k's step i, i < min(n_steps[k], capacity)."""
+    steps: np.ndarray
+    n_steps: np.ndarray
+    stop_reason: np.ndarray
+    status: np.ndarray
+
+    def ray(self, k: int) -> np.ndarray:
+        return self.steps[k, : min(int(self.n_steps[k]), self.steps.shape[1])]
+
+
+def ray_at(geometry: int, radius: float, a: float, position, direction):
+    """render_ray_at's initial (position, momentum) in the geometry's chart (grt_ray_at)."""
+    p, d = np.ascontiguousarray(position, np.float64), np.ascontiguousarray(direction, np.float64)
+    po, mo = np.zeros(4), np.zeros(4)
+    L.check(L.lib().grt_ray_at(geometry, radius, a, L.dptr(p), L.dptr(d), L.dptr(po), L.dptr(mo)), "grt_ray_at")
+    return po, mo
+
+
+def write_trajectory_csv(path: str, geometry: int, a: float, records) -> None:
+    """IntegratedRay::save (ray.rs:35-54) of (n, 9) records."""
+    r = np.ascontiguousarray(records, np.float64).reshape(-1, 9)
+    L.check(L.lib().grt_write_trajectory_csv(str(path).encode(), geometry, a, L.dptr(r), r.shape[0]),
+            "grt_write_trajectory_csv")
+
+
+def format_f64(v: float) -> str:
+    """Rust's Display of an f64 (shortest round-trip digits, positional)."""
+    buf = C.create_string_buffer(1200)
+    L.lib().grt_format_f64(float(v), buf, 1200)
+    return buf.value.decode()
 
 
 def r_isco(radius: float, a: float) -> float:

@@ -211,6 +211,10 @@ void grt_default_adaptive_config(grt_adaptive_config* cfg);
  * Texture paths are resolved relative to `resource_root` (NULL = cwd). */
 int grt_host_scene_load(const char* toml_path, const char* resource_root,
                         const grt_global_opts* opts, grt_host_scene** out);
+/* Geometry and integration configuration only (no camera, textures or objects): what
+ * `render-ray-at` uses (main.rs:143-168 builds the geometry, not a scene). */
+int grt_host_geometry_load(const char* toml_path, const grt_global_opts* opts,
+                           grt_host_scene** out);
 const grt_scene_desc* grt_host_scene_desc(const grt_host_scene* s);
 void grt_host_scene_adaptive(const grt_host_scene* s, grt_adaptive_config* out);
 int grt_host_scene_destroy(grt_host_scene* s);
@@ -339,6 +343,37 @@ int grt_render_shard(grt_scene* scene, int device, const grt_row_shard* sh, floa
 int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt_row_shard* sh,
                            float* d_xyza, uint8_t* d_class, uint8_t* d_status, double* d_xyza64,
                            uint32_t* d_steps, uint8_t* d_stop, uint64_t* d_stats);
+
+/* ---- whole trajectories (render-ray / render-ray-at) ------ */
+/* Integrator::integrate keeping every Step (integrator.rs:78-174), as
+ * Raytracer::integrate_ray_at_point (raytracer.rs:499-507, `render-ray`) and
+ * integrate_and_save_ray (cli/shared.rs:107-129, `render-ray-at`) use it.  Ray k's
+ * records are steps_out[(k * capacity + i) * 9 + f], i = 0 .. min(n_steps[k], capacity)
+ * - 1, f = 0: affine parameter t; 1..4: position x^mu in the geometry's own chart;
+ * 5..8: momentum_from_state p^mu.  Record 0 is the initial state.  n_steps[k] counts
+ * every step, also those beyond `capacity`; stop_out is a grt_stop_reason, status_out a
+ * grt_status (GRT_ERR_MAX_STEPS_REACHED: rkf45's Err, the reference writes no CSV). */
+int grt_trace_pixels(grt_scene* scene, int device, uint64_t n, const double* rows,
+                     const double* cols, uint64_t capacity, double* steps_out,
+                     uint64_t* n_steps, uint8_t* stop_out, uint8_t* status_out);
+/* Rays given by position and contravariant momentum in the geometry's chart (n x 4). */
+int grt_trace_rays(grt_scene* scene, int device, uint64_t n, const double* positions,
+                   const double* momenta, uint64_t capacity, double* steps_out,
+                   uint64_t* n_steps, uint8_t* stop_out, uint8_t* status_out);
+
+/* render_ray_at's initial ray (cli/{euclidean,schwarzschild,kerr,kerr_bl}.rs): the unit
+ * spatial `direction` in the local tetrad at the Cartesian `position` (t = 0), as a
+ * native-chart position and contravariant momentum for grt_trace_rays.  -EINVAL when
+ * the direction is degenerate or the momentum is not future-directed
+ * (assert_future_directed, cli/shared.rs:79-86). */
+int grt_ray_at(int32_t geometry, double radius, double a, const double position[3],
+               const double direction[3], double position_out[4], double momentum_out[4]);
+/* IntegratedRay::save (ray.rs:35-54): "i,t,tau,x,y,z" then one line per record
+ * (step, t, Cartesian x^0..x^3), f64 printed like Rust's Display. */
+int grt_write_trajectory_csv(const char* path, int32_t geometry, double a, const double* steps,
+                             uint64_t n_records);
+/* Rust Display of one f64 into buf (NUL-terminated, truncated to cap); returns its length. */
+size_t grt_format_f64(double v, char* buf, size_t cap);
 
 /* ---- device output stage ------------------------------- */
 /* Replaces xyz_to_linear_srgb_buffer + linear_srgb_to_srgb_buffer (color.rs:204-298),

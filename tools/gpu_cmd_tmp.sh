@@ -1,3 +1,4 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python3 -m pytest tests/test_output_stage.py -m gpu -q -rA -p no:cacheprovider > gpurun_out/out_stage.log 2>&1
+timeout -k 10 600 python3 -m pytest tests/test_trajectory.py -m gpu -q -rA -p no:cacheprovider > gpurun_out/traj.log 2>&1
+echo "pytest rc=$?"
