@@ -25,6 +25,8 @@ namespace {
 
 int g_blocks_per_cu = 0;
 int g_threads = 256;
+int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
+constexpr uint32_t PROBE_CAP = 32768;  // > the ~1.6e4 steps of an escaping ray at H_MAX
 
 int fail(int code, const std::string& msg) {
   grt_host::set_error(msg);
@@ -54,6 +56,9 @@ struct DeviceCopy {
   // integrate -> shade hand-off buffers, grown on demand (bytes per ray: ~1.1 KB)
   uint64_t ws_cap = 0;
   void* ws_mem = nullptr;
+  // tile-order scratch (probe counts, keys, indices, order, radix-sort temp), grow-only
+  uint64_t sched_tiles = 0;
+  void* sched_mem = nullptr;
 };
 
 // Carve a Workspace for n rays out of the device's grow-only arena.
@@ -292,9 +297,61 @@ grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_
   return wl;
 }
 
+// Probe-ordered tile queue (schedule.hip): worth its ~1/64 extra rays when a ray may run
+// far longer than an escaping one (max_steps well above the probe cap) over many tiles.
+bool schedule_wanted(const grt_scene* s, const grt::WorkList& wl) {
+  if (wl.pixel_index || g_schedule == 0) return false;
+  const uint64_t tiles = wl.n_items / 64;
+  if (g_schedule == 1) return tiles > 1;
+  return s->desc.max_steps >= 8ull * PROBE_CAP && tiles >= 1024;
+}
+
+// Enqueue the probe pass and the sort; returns the device tile order in *order.
+int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hipStream_t stream,
+                       const uint32_t** order) {
+  const uint32_t tiles_x = wl.tiles_x, tiles_y = (uint32_t)(wl.n_items / 64 / wl.tiles_x);
+  const uint64_t n = (uint64_t)tiles_x * tiles_y;
+  size_t temp_bytes = 0;
+  HIP_TRY(grt::launch_tile_order(nullptr, tiles_x, tiles_y, nullptr, nullptr, nullptr, nullptr, nullptr, &temp_bytes,
+                                 stream));
+  const uint64_t need = 5 * ((n * 4 + 255) & ~255ull) + temp_bytes + 256;
+  if (n > dc.sched_tiles || !dc.sched_mem) {
+    if (dc.sched_mem) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(dc.sched_mem);
+      dc.sched_mem = nullptr;
+    }
+    dc.sched_tiles = 0;
+    // room for a frame of the same tile count with a larger radix-sort temp
+    HIP_TRY(hipMalloc(&dc.sched_mem, need + (need >> 2)));
+    dc.sched_tiles = n;
+  }
+  char* p = (char*)dc.sched_mem;
+  auto take = [&](uint64_t bytes) {
+    char* r = p;
+    p += (bytes + 255) & ~255ull;
+    return r;
+  };
+  uint32_t* probe = (uint32_t*)take(n * 4);
+  uint32_t* keys = (uint32_t*)take(n * 4);
+  uint32_t* keys_sorted = (uint32_t*)take(n * 4);
+  uint32_t* idx = (uint32_t*)take(n * 4);
+  uint32_t* ord = (uint32_t*)take(n * 4);
+  void* temp = take(temp_bytes);
+  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, PROBE_CAP, probe, stream));
+  HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, keys, keys_sorted, idx, ord, temp, &temp_bytes, stream));
+  *order = ord;
+  return 0;
+}
+
 // Enqueue one trace over `wl` on `stream`; counters are zeroed first.
-int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, const grt::Outputs& o,
+int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, const grt::Outputs& o,
                   unsigned long long* d_stats, hipStream_t stream) {
+  grt::WorkList wl = wl_in;
+  if (schedule_wanted(s, wl)) {
+    int rc0 = enqueue_tile_order(s, dc, wl, stream, &wl.tile_order);
+    if (rc0) return rc0;
+  }
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
   int threads = g_threads;
   int blocks = g_blocks_per_cu > 0 ? dc.cus * g_blocks_per_cu : dc.blocks;
@@ -365,6 +422,12 @@ int grt_set_launch_config(int blocks_per_cu, int threads_per_block) {
   return 0;
 }
 
+int grt_set_schedule(int mode) {
+  if (mode < -1 || mode > 1) return fail(-EINVAL, "schedule mode must be -1 (auto), 0 or 1");
+  g_schedule = mode;
+  return 0;
+}
+
 int grt_scene_create(const grt_scene_desc* desc, grt_scene** out) {
   if (!out) return fail(-EINVAL, "null output pointer");
   int rc = validate_desc(desc);
@@ -405,6 +468,7 @@ int grt_scene_destroy(grt_scene* s) {
     (void)hipSetDevice((int)dev);
     for (void* p : dc->allocations) (void)hipFree(p);
     if (dc->ws_mem) (void)hipFree(dc->ws_mem);
+    if (dc->sched_mem) (void)hipFree(dc->sched_mem);
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
     delete dc;

@@ -86,6 +86,7 @@ struct WorkList {
   const uint32_t* pixel_index;  // offsets mode (NULL = rectangle mode)
   const double* dx;
   const double* dy;
+  const uint32_t* tile_order;   // rectangle mode: queue position -> tile (NULL = row-major)
 };
 
 // Hand-off from the integrate kernel to the shade kernel, structure-of-arrays with

@@ -1003,6 +1003,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
             idx = item;
           } else {  // 8x8 pixel tiles, row-major tiles: a wave starts on a compact patch
             uint64_t tile = item >> 6;
+            if (wl.tile_order) tile = wl.tile_order[tile];  // longest-predicted tiles first
             uint32_t w = (uint32_t)(item & 63);
             uint32_t tr = (uint32_t)(tile / wl.tiles_x), tc = (uint32_t)(tile % wl.tiles_x);
             uint32_t r = tr * 8 + (w >> 3), cc = tc * 8 + (w & 7);
@@ -1205,6 +1206,74 @@ hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const Traj
       break;
     case GRT_GEOM_KERR_BL:
       hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, tl);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ============================================================ probe kernel =======
+// Work-order probe (scheduling only, never an output): one ray per 8x8 tile, the
+// tile's pixel (3, 3), integrated for at most `cap` accepted steps.  A frame's cost is
+// heavy-tailed where rays spiral into the horizon or orbit near the photon sphere
+// (C4: 6% of the rays carry 60% of the steps, up to max_steps each); with the counts
+// the host queues the long tiles first, so the frame does not end on a lone ray that
+// started late.  Writes the steps taken (cap if the probe had not finished).
+template <int G>
+__global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ Sp, WorkList wl, uint32_t n_tiles,
+                                                   uint32_t cap, uint32_t* __restrict__ steps_out) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles) return;
+  const uint32_t tr = t / wl.tiles_x, tc = t % wl.tiles_x;
+  const uint32_t r = min(tr * 8 + 3, wl.rows - 1), c = min(tc * 8 + 3, wl.cols - 1);
+  double y[8];
+  RayConst rc;
+  init_ray<G>(S, (double)(wl.row0 + shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, r)),
+              (double)(wl.col0 + c), y, rc);
+  const uint64_t end = S.max_steps < (uint64_t)cap ? S.max_steps : (uint64_t)cap;
+  uint64_t i = 1;
+  double h = S.step_size;
+  for (; i < end; ++i) {
+    double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
+    int retries = 0, ctl;
+    do {
+      const double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
+      ctl = step_control(S, err, h_cur, retries, h_next);
+    } while (ctl == STEP_RETRY);
+    if (ctl == STEP_FAILED) break;
+    h = h_next;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = yn[k];
+    double cc[3];
+    bool c_valid = false;
+    if (should_stop<G>(S, y, cc, c_valid, i) != GRT_STOP_NONE) break;
+  }
+  steps_out[t] = (uint32_t)(i < end ? i : cap);
+}
+
+hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,
+                        uint32_t* d_steps, hipStream_t stream) {
+  if (n_tiles == 0) return hipSuccess;
+  const unsigned blocks = (n_tiles + 63) / 64;
+  switch (geometry) {
+    case GRT_GEOM_EUCLIDEAN:
+      hipLaunchKernelGGL(probe_kernel<GRT_GEOM_EUCLIDEAN>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n_tiles,
+                         cap, d_steps);
+      break;
+    case GRT_GEOM_SCHWARZSCHILD:
+      hipLaunchKernelGGL(probe_kernel<GRT_GEOM_SCHWARZSCHILD>, dim3(blocks), dim3(64), 0, stream, d_scene, wl,
+                         n_tiles, cap, d_steps);
+      break;
+    case GRT_GEOM_KERR:
+      hipLaunchKernelGGL(probe_kernel<GRT_GEOM_KERR>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n_tiles, cap,
+                         d_steps);
+      break;
+    case GRT_GEOM_KERR_BL:
+      hipLaunchKernelGGL(probe_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n_tiles,
+                         cap, d_steps);
       break;
     default:
       return hipErrorInvalidValue;

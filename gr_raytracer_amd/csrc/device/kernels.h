@@ -11,6 +11,15 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
                         int blocks, int threads, hipStream_t stream);
 
+// Work-order probe: steps of one ray per 8x8 tile of `wl` (rectangle mode), capped.
+hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,
+                        uint32_t* d_steps, hipStream_t stream);
+// Tile queue order from the probe counts (schedule.hip): 3x3-dilated counts, sorted
+// descending (stable).  `temp` / `temp_bytes`: scratch, query with temp == NULL.
+hipError_t launch_tile_order(const uint32_t* d_probe, uint32_t tiles_x, uint32_t tiles_y, uint32_t* d_keys,
+                             uint32_t* d_keys_sorted, uint32_t* d_idx, uint32_t* d_order, void* temp,
+                             size_t* temp_bytes, hipStream_t stream);
+
 // Whole trajectories (render-ray / render-ray-at): camera pixels (row, col) or explicit
 // native-chart (position, momentum) pairs; record layout in trajectory_kernel.
 struct TrajectoryList {

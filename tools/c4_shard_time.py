@@ -13,6 +13,11 @@ opts = g.GlobalOpts(width=4096, height=4096, camera_position=(-10.0, 0.0, -0.5),
                     max_steps=1000000)
 hs = g.HostScene(str(ROOT / "tests/golden/scenes/kerr.toml"), opts, str(ROOT / "tests/golden"))
 sc = g.Scene(hs.desc_ptr(), keepalive=hs)
+import os  # noqa: E402
+from gr_raytracer_amd import _lib as L  # noqa: E402
+if "GRT_SCHEDULE" in os.environ:  # -1 auto, 0 row-major tiles, 1 probe-ordered
+    L.check(L.lib().grt_set_schedule(int(os.environ["GRT_SCHEDULE"])))
+import hashlib  # noqa: E402
 n_shards = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 shards = [int(x) for x in sys.argv[2:]] or [0, n_shards // 2]
 for s in shards:
@@ -22,4 +27,5 @@ for s in shards:
     print(json.dumps({"shard": s, "n_shards": n_shards, "rays": st["rays"], "wall_s": round(time.time() - t, 3),
                       "kernel_ms": st["kernel_ms"], "accepted": st["accepted_steps"], "attempts": st["attempts"],
                       "steps_per_s": st["accepted_steps"] / (st["kernel_ms"] * 1e-3),
-                      "overflows": st["hit_overflows"]}), flush=True)
+                      "overflows": st["hit_overflows"], "schedule": os.environ.get("GRT_SCHEDULE", "auto"),
+                      "md5": hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12]}), flush=True)
