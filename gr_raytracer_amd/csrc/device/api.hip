@@ -298,12 +298,17 @@ grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_
 }
 
 // Probe-ordered tile queue (schedule.hip): worth its ~1/64 extra rays when a ray may run
-// far longer than an escaping one (max_steps well above the probe cap) over many tiles.
+// far longer than an escaping one (max_steps well above the probe cap) over many tiles,
+// in the affine-parameter charts.  KerrBL integrates in Mino time, where even captured
+// rays take ~1e3 steps (C3: max 1147), and Euclidean rays are straight lines: there the
+// probe pass is pure overhead (measured +5% on C3), so automatic mode skips them.
 bool schedule_wanted(const grt_scene* s, const grt::WorkList& wl) {
   if (wl.pixel_index || g_schedule == 0) return false;
   const uint64_t tiles = wl.n_items / 64;
   if (g_schedule == 1) return tiles > 1;
-  return s->desc.max_steps >= 8ull * PROBE_CAP && tiles >= 1024;
+  const int g = s->desc.geometry;
+  return (g == GRT_GEOM_KERR || g == GRT_GEOM_SCHWARZSCHILD) && s->desc.max_steps >= 8ull * PROBE_CAP &&
+         tiles >= 1024;
 }
 
 // Enqueue the probe pass and the sort; returns the device tile order in *order.

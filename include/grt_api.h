@@ -396,7 +396,8 @@ int grt_xyz_to_srgb8_device(int device, const double* xyza, size_t n, int32_t to
 int grt_set_launch_config(int blocks_per_cu, int threads_per_block);
 /* Tile queue order of rectangle / shard traces: 0 = row-major 8x8 tiles; 1 = a probe
  * pass (one capped ray per tile) then the tiles with the longest predicted rays first;
- * -1 = automatic (default: probe order when max_steps >= 262144 over >= 1024 tiles).
+ * -1 = automatic (default: probe order for Kerr-Schild / Schwarzschild when
+ * max_steps >= 262144 over >= 1024 tiles; KerrBL's Mino-time rays are all short).
  * Scheduling only: every pixel's result is identical in all modes. */
 int grt_set_schedule(int mode);
 

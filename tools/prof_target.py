@@ -4,6 +4,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import gr_raytracer_amd as g
+import os
+if "GRT_SCHEDULE" in os.environ:  # -1 auto, 0 row-major tiles, 1 probe-ordered
+    g.lib().grt_set_schedule(int(os.environ["GRT_SCHEDULE"]))
 which = sys.argv[1] if len(sys.argv) > 1 else "c2"
 if which == "c2":
     opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, max_steps=100000)
