@@ -155,6 +155,8 @@ def lib() -> C.CDLL:
         "grt_srgb_to_xyza": (None, [C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8, _pd]),
         "grt_xyz_to_srgb8": (C.c_int, [_pd, C.c_size_t, i32, _d, C.POINTER(C.c_uint8)]),
         "grt_linear_max": (None, [_pd, C.c_size_t, _d, _pd]),
+        "grt_xyz_to_srgb": (None, [_pd, _d, C.POINTER(C.c_uint8)]),
+        "grt_blackbody_spectrum": (C.c_int, [_d, _d, _d, _d, u32, u32, i32, C.POINTER(C.c_uint8)]),
         "grt_tonemap": (C.c_int, [_pd, C.c_size_t, i32, _d, _pd, C.POINTER(C.c_uint8)]),
         "grt_scene_create": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(vp)]),
         "grt_scene_destroy": (C.c_int, [vp]),
@@ -200,7 +202,7 @@ EXPORTED_SYMBOLS = [
     "grt_host_scene_load", "grt_host_geometry_load", "grt_host_scene_desc", "grt_host_scene_adaptive", "grt_host_scene_destroy",
     "grt_camera_build", "grt_stationary_velocity", "grt_zamo_velocity", "grt_cartesian_to_spherical",
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
-    "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_xyz_to_srgb8", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
+    "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_xyz_to_srgb8", "grt_xyz_to_srgb", "grt_blackbody_spectrum", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
     "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config", "grt_set_schedule",
     "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",

@@ -9,6 +9,9 @@
 //              [--to-row N] [--to-col N]
 //     | render-ray -r ROW -c COL [--filename rendered-ray.csv]
 //     | render-ray-at -p x,y,z -d x,y,z [--filename rendered-ray-at.csv]
+//     | blackbody -t T [-r Z]
+//     | blackbody-spectrum [--min-temperature T] [--max-temperature T] [--min-redshift Z]
+//                          [--max-redshift Z] [--width N] [--height N] [-f FILE]
 //
 // Global options go before the subcommand, subcommand options after it (clap).
 // Extra (not in the reference): --device N selects the GPU, --resource-root DIR
@@ -25,6 +28,8 @@
 
 namespace grt_host {
 bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err);
+bool png_encode_rgba(const std::string& path, const uint8_t* rgba, uint32_t w, uint32_t h, std::string& err);
+std::string rust_display_f64(double v);
 bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint32_t h, std::string& err);
 }
 
@@ -32,7 +37,10 @@ static int usage(const char* msg) {
   std::fprintf(stderr,
                "error: %s\nusage: grt [global options] --config-file FILE render [--filename F]\n"
                "       grt [global options] --config-file FILE render-ray -r ROW -c COL [--filename F]\n"
-               "       grt [global options] --config-file FILE render-ray-at -p X,Y,Z -d X,Y,Z [--filename F]\n",
+               "       grt [global options] --config-file FILE render-ray-at -p X,Y,Z -d X,Y,Z [--filename F]\n"
+               "       grt [global options] blackbody -t T [-r Z]\n"
+               "       grt [global options] blackbody-spectrum [--min-temperature T] [--max-temperature T]\n"
+               "           [--min-redshift Z] [--max-redshift Z] [--width N] [--height N] [-f FILE]\n",
                msg);
   return 2;
 }
@@ -106,6 +114,10 @@ int main(int argc, char** argv) {
   bool have_row = false, have_col = false;
   std::vector<double> ray_position, ray_direction;
   bool have_position = false, have_direction = false;
+  // blackbody / blackbody-spectrum (cli.rs:88-110 defaults)
+  double bb_temperature = 0.0, bb_redshift = 1.0, bb_tmin = 1000.0, bb_tmax = 10000.0, bb_zmin = 0.5, bb_zmax = 2.0;
+  uint32_t bb_w = 1000, bb_h = 1000;
+  bool have_temperature = false;
   int device = 0;
   std::vector<std::string> args(argv + 1, argv + argc);
   for (size_t i = 0; i < args.size(); ++i) {
@@ -127,12 +139,11 @@ int main(int argc, char** argv) {
       return true;
     };
     std::string v;
-    if (action.empty() && (a == "render" || a == "render-ray" || a == "render-ray-at")) {
+    if (action.empty() && (a == "render" || a == "render-ray" || a == "render-ray-at" || a == "blackbody" ||
+                           a == "blackbody-spectrum")) {
       action = a;
       continue;
     }
-    if (action.empty() && (a == "blackbody" || a == "blackbody-spectrum"))
-      return usage(("subcommand '" + a + "' is outside this build's hot-path scope").c_str());
     if (action.empty() && a == "--show-sampling-mask") { opts.show_sampling_mask = 1; continue; }
     if (!next(v)) return usage(("missing value for " + a).c_str());
     std::vector<double> nums;
@@ -154,7 +165,18 @@ int main(int argc, char** argv) {
       } else if (action == "render-ray-at" && (a == "-d" || a == "--direction")) {
         if (!split_csv(v, ray_direction)) return usage("invalid direction");
         have_direction = true;
-      } else return usage(("unknown argument " + a + " for " + action).c_str());
+      } else if (action == "blackbody" && (a == "-t" || a == "--temperature")) {
+        bb_temperature = std::atof(v.c_str());
+        have_temperature = true;
+      } else if (action == "blackbody" && (a == "-r" || a == "--redshift")) bb_redshift = std::atof(v.c_str());
+      else if (action == "blackbody-spectrum" && a == "--min-temperature") bb_tmin = std::atof(v.c_str());
+      else if (action == "blackbody-spectrum" && a == "--max-temperature") bb_tmax = std::atof(v.c_str());
+      else if (action == "blackbody-spectrum" && a == "--min-redshift") bb_zmin = std::atof(v.c_str());
+      else if (action == "blackbody-spectrum" && a == "--max-redshift") bb_zmax = std::atof(v.c_str());
+      else if (action == "blackbody-spectrum" && a == "--width") bb_w = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
+      else if (action == "blackbody-spectrum" && a == "--height") bb_h = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
+      else if (action == "blackbody-spectrum" && a == "-f") filename = v;
+      else return usage(("unknown argument " + a + " for " + action).c_str());
       continue;
     }
     if (a == "--width") opts.width = std::atoll(v.c_str());
@@ -182,7 +204,36 @@ int main(int argc, char** argv) {
     } else if (a == "-c" || a == "--config-file") config_file = v;
     else return usage(("unknown argument " + a).c_str());
   }
-  if (action.empty()) return usage("missing subcommand (render, render-ray, render-ray-at)");
+  if (action.empty()) return usage("missing subcommand (render, render-ray, render-ray-at, blackbody, blackbody-spectrum)");
+  if (action == "blackbody") {  // run_blackbody (cli/blackbody.rs:7-25): no scene needed
+    if (!have_temperature) return usage("blackbody needs --temperature");
+    double xyz[3];
+    uint8_t c[3];
+    grt_blackbody_xyz(bb_temperature, bb_redshift, xyz);
+    grt_xyz_to_srgb(xyz, 1.0, c);
+    std::printf("Blackbody color at T=%sK (redshift=%s):\n", grt_host::rust_display_f64(bb_temperature).c_str(),
+                grt_host::rust_display_f64(bb_redshift).c_str());
+    std::printf("XYZ:  %.4f, %.4f, %.4f\n", xyz[0], xyz[1], xyz[2]);
+    std::printf("sRGB: R=%u, G=%u, B=%u\n", c[0], c[1], c[2]);
+    std::printf("sRGB: R=%.4f, G=%.4f, B=%.4f\n", c[0] / 255.0, c[1] / 255.0, c[2] / 255.0);
+    std::printf("Color block: \x1b[48;2;%u;%u;%um      \x1b[0m\n", c[0], c[1], c[2]);
+    return 0;
+  }
+  if (action == "blackbody-spectrum") {  // run_blackbody_spectrum (cli/blackbody.rs:27-95)
+    if (filename.empty()) filename = "blackbody_spectrum.png";
+    std::vector<uint8_t> rgba((size_t)bb_w * bb_h * 4);
+    if (grt_blackbody_spectrum(bb_tmin, bb_tmax, bb_zmin, bb_zmax, bb_w, bb_h, opts.tone_mapping, rgba.data())) {
+      std::fprintf(stderr, "Error: %s\n", grt_last_error());
+      return 1;
+    }
+    std::string err;
+    if (!grt_host::png_encode_rgba(filename, rgba.data(), bb_w, bb_h, err)) {
+      std::fprintf(stderr, "Failed to save spectrum image: %s\n", err.c_str());
+      return 1;
+    }
+    std::printf("Saved blackbody spectrum to %s\n", filename.c_str());
+    return 0;
+  }
   if (action == "render-ray" && !(have_row && have_col)) return usage("render-ray needs --row and --col");
   if (action == "render-ray-at" && !(have_position && have_direction))
     return usage("render-ray-at needs --position and --direction");

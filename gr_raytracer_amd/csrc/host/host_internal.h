@@ -27,6 +27,7 @@ int blackbody_lut(uint32_t n, double* log_t, double* xyz);
 double inv_compand_srgb(double u);
 void srgb_to_xyza(uint8_t r8, uint8_t g8, uint8_t b8, uint8_t a8, double out[4]);
 int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_t* rgb);
+void xyz_to_srgb(const double* xyz, double exposure, uint8_t* rgb);
 void linear_max(const double* xyza, size_t n, double exposure, double* max3);
 int tonemap(const double* xyza, size_t n, int tone, double exposure, const double* max3, uint8_t* rgb);
 int stationary(int geometry, double radius, double a, const double position[4], double out[4]);
@@ -34,6 +35,8 @@ int zamo(int geometry, double radius, double a, const double position[4], double
 int ray_at(int geometry, double radius, double a, const double position[3], const double direction[3],
            double pos_out[4], double mom_out[4], std::string& err);
 std::string rust_display_f64(double v);
+int blackbody_spectrum(double t_min, double t_max, double z_min, double z_max, uint32_t w, uint32_t h, int tone,
+                       uint8_t* rgba);
 
 // ---- minimal TOML (the subset the reference's scene files use) ----
 struct TomlValue;
@@ -54,6 +57,7 @@ bool toml_parse(const std::string& text, TomlTable& root, std::string& err);
 bool png_decode_rgba(const std::string& path, std::vector<uint8_t>& rgba, uint32_t& w, uint32_t& h,
                      std::string& err);
 bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err);
+bool png_encode_rgba(const std::string& path, const uint8_t* rgba, uint32_t w, uint32_t h, std::string& err);
 bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint32_t h, std::string& err);
 
 }  // namespace grt_host

@@ -150,11 +150,14 @@ static void chunk(std::vector<uint8_t>& out, const char* type, const std::vector
   put32(out, (uint32_t)crc32(0, td.data(), (uInt)td.size()));
 }
 
-bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err) {
-  std::vector<uint8_t> raw(((size_t)w * 3 + 1) * h);
+// 8-bit RGB (colour type 2) or RGBA (6), no interlace, filter 0 on every row.
+static bool png_encode(const std::string& path, const uint8_t* px, uint32_t w, uint32_t h, uint32_t channels,
+                       std::string& err) {
+  const size_t row = (size_t)w * channels;
+  std::vector<uint8_t> raw((row + 1) * h);
   for (uint32_t y = 0; y < h; ++y) {
-    raw[y * (w * 3 + 1)] = 0;
-    std::memcpy(&raw[y * (w * 3 + 1) + 1], rgb + (size_t)y * w * 3, (size_t)w * 3);
+    raw[y * (row + 1)] = 0;
+    std::memcpy(&raw[y * (row + 1) + 1], px + (size_t)y * row, row);
   }
   uLongf zl = compressBound((uLong)raw.size());
   std::vector<uint8_t> z(zl);
@@ -167,7 +170,7 @@ bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uin
   std::vector<uint8_t> ihdr;
   put32(ihdr, w);
   put32(ihdr, h);
-  ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});
+  ihdr.insert(ihdr.end(), {8, (uint8_t)(channels == 4 ? 6 : 2), 0, 0, 0});
   chunk(out, "IHDR", ihdr);
   chunk(out, "IDAT", z);
   chunk(out, "IEND", {});
@@ -178,6 +181,13 @@ bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uin
   }
   f.write((const char*)out.data(), (std::streamsize)out.size());
   return (bool)f;
+}
+
+bool png_encode_rgb(const std::string& path, const uint8_t* rgb, uint32_t w, uint32_t h, std::string& err) {
+  return png_encode(path, rgb, w, h, 3, err);
+}
+bool png_encode_rgba(const std::string& path, const uint8_t* rgba, uint32_t w, uint32_t h, std::string& err) {
+  return png_encode(path, rgba, w, h, 4, err);
 }
 
 bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint32_t h, std::string& err) {

@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "grt_api.h"
@@ -727,6 +728,39 @@ void blackbody_xyz(double temperature, double redshift, double out[3]) {  // bla
   out[2] = za * boost;
 }
 
+// run_blackbody_spectrum (cli/blackbody.rs:27-95): a width x height image of the
+// redshifted blackbody colour, temperature along x and redshift along y, through the
+// output stage (exposure 1, the CLI's tone mapping), RGBA with alpha 255.  Host threads
+// stand in for the reference's rayon loop; each pixel is independent.
+int blackbody_spectrum(double t_min, double t_max, double z_min, double z_max, uint32_t w, uint32_t h, int tone,
+                       uint8_t* rgba) {
+  const size_t n = (size_t)w * h;
+  std::vector<double> xyza(4 * n);
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> pool;
+  for (unsigned k = 0; k < nt; ++k)
+    pool.emplace_back([&, k] {
+      for (size_t i = k; i < n; i += nt) {
+        const double x = (double)(i % w), y = (double)(i / w);
+        const double temperature = t_min + x * (t_max - t_min) / ((double)w - 1.0);
+        const double redshift = z_min + y * (z_max - z_min) / ((double)h - 1.0);
+        blackbody_xyz(temperature, redshift, &xyza[4 * i]);
+        xyza[4 * i + 3] = 1.0;
+      }
+    });
+  for (auto& t : pool) t.join();
+  std::vector<uint8_t> rgb(3 * n);
+  int rc = xyz_to_srgb8(xyza.data(), n, tone, 1.0, rgb.data());
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    rgba[4 * i] = rgb[3 * i];
+    rgba[4 * i + 1] = rgb[3 * i + 1];
+    rgba[4 * i + 2] = rgb[3 * i + 2];
+    rgba[4 * i + 3] = 255;
+  }
+  return 0;
+}
+
 int blackbody_lut(uint32_t n, double* log_t, double* xyz) {  // texture.rs:121-138
   if (n < 2) return -EINVAL;
   double min_log = std::log10(10.0), max_log = std::log10(10000000.0);
@@ -819,6 +853,12 @@ int tonemap(const double* xyza, size_t n, int tone, double exposure, const doubl
   }
   return 0;
 }
+// xyz_to_srgb (color.rs:225-241): one colour, linear sRGB * exposure, no tone mapping.
+void xyz_to_srgb(const double* xyz, double exposure, uint8_t* rgb) {
+  double lin[3];
+  to_linear(xyz, lin);
+  for (int k = 0; k < 3; ++k) rgb[k] = to_u8(compand_srgb(std::fmax(lin[k] * exposure, 0.0)));
+}
 int xyz_to_srgb8(const double* xyza, size_t n, int tone, double exposure, uint8_t* rgb) {
   double m[3] = {0.0, 0.0, 0.0};
   if (tone == GRT_TONE_GLOBAL_LINEAR) linear_max(xyza, n, exposure, m);
@@ -899,6 +939,17 @@ int grt_ray_at(int32_t geometry, double radius, double a, const double position[
   std::string err;
   int rc = grt_host::ray_at(geometry, radius, a, position, direction, position_out, momentum_out, err);
   if (rc) grt_host::set_error(err);
+  return rc;
+}
+void grt_xyz_to_srgb(const double xyz[3], double exposure, uint8_t rgb_out[3]) {
+  grt_host::xyz_to_srgb(xyz, exposure, rgb_out);
+}
+int grt_blackbody_spectrum(double min_temperature, double max_temperature, double min_redshift, double max_redshift,
+                           uint32_t width, uint32_t height, int32_t tone_mapping, uint8_t* rgba_out) {
+  if (!rgba_out && (size_t)width * height != 0) return -EINVAL;
+  int rc = grt_host::blackbody_spectrum(min_temperature, max_temperature, min_redshift, max_redshift, width, height,
+                                        tone_mapping, rgba_out);
+  if (rc) grt_host::set_error("grt_blackbody_spectrum: unknown tone mapping");
   return rc;
 }
 void grt_linear_max(const double* xyza, size_t n, double exposure, double max3[3]) {

@@ -248,6 +248,15 @@ int grt_blackbody_lut(uint32_t n, double* log_t, double* xyz);
 void grt_blackbody_xyz(double temperature, double redshift, double out_xyz[3]);
 /* srgb_to_xyz (color.rs:310-332), alpha := a/255 (CIETristimulus::from_color). */
 void grt_srgb_to_xyza(uint8_t r, uint8_t g, uint8_t b, uint8_t a, double out[4]);
+/* xyz_to_srgb (color.rs:225-241): one XYZ colour -> sRGB8, linear * exposure, no
+ * tone mapping (the `blackbody` subcommand, cli/blackbody.rs:7-25). */
+void grt_xyz_to_srgb(const double xyz[3], double exposure, uint8_t rgb_out[3]);
+/* run_blackbody_spectrum (cli/blackbody.rs:27-95): width x height RGBA8 image of
+ * integrate_blackbody_xyz(T, z), T linear in x over [min, max] temperature, z linear
+ * in y over [min, max] redshift, tone-mapped like a render (exposure 1), alpha 255. */
+int grt_blackbody_spectrum(double min_temperature, double max_temperature, double min_redshift,
+                           double max_redshift, uint32_t width, uint32_t height,
+                           int32_t tone_mapping, uint8_t* rgba_out);
 /* xyz -> tone-mapped sRGB8 (color.rs:204-298), whole buffer = grt_linear_max (only for
  * GlobalLinear) + grt_tonemap.  Split so that a frame spread over several processes
  * can reduce the three channel maxima (MAX) before mapping its own rows. */
