@@ -17,7 +17,7 @@ GRT_MAX_OBJECTS = 8
 GRT_MAX_HITS = 16
 
 # enums (grt_api.h)
-GEOM_EUCLIDEAN, GEOM_SCHWARZSCHILD, GEOM_KERR, GEOM_KERR_BL = 0, 1, 2, 3
+GEOM_EUCLIDEAN, GEOM_SCHWARZSCHILD, GEOM_KERR, GEOM_KERR_BL, GEOM_EUCLIDEAN_SPHERICAL = 0, 1, 2, 3, 4
 TEX_BITMAP, TEX_CHECKER, TEX_BLACKBODY = 0, 1, 2
 OBJ_SPHERE, OBJ_DISC = 0, 1
 TEMP_CONSTANT, TEMP_KERR_LUT = 0, 1

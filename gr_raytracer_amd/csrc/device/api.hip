@@ -185,7 +185,8 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   // Far-field filter bounds.  The margins (1e-9 relative) are ~1e6 x the rounding of
   // the Cartesian conversion and of the chord arithmetic, so every window the filter
   // skips would have been a miss in the reference too ("Exact skips").
-  ds.far_ok = (d.geometry == GRT_GEOM_SCHWARZSCHILD || d.geometry == GRT_GEOM_KERR_BL) ? 1 : 0;
+  ds.far_ok = (d.geometry == GRT_GEOM_SCHWARZSCHILD || d.geometry == GRT_GEOM_KERR_BL ||
+               d.geometry == GRT_GEOM_EUCLIDEAN_SPHERICAL) ? 1 : 0;
   ds.far_a = d.geometry == GRT_GEOM_KERR_BL ? std::fabs(d.a) : 0.0;
   ds.cel_lo2 = ds.max_radius_sq * (1.0 - 1e-9);
   ds.cel_hi2 = ds.max_radius_sq * (1.0 + 1e-9);
@@ -387,7 +388,8 @@ struct DevBuf {
 int validate_desc(const grt_scene_desc* d) {
   if (!d) return fail(-EINVAL, "null scene descriptor");
   if (d->abi_version != GRT_ABI_VERSION) return fail(-EINVAL, "grt_scene_desc ABI version mismatch");
-  if (d->geometry < GRT_GEOM_EUCLIDEAN || d->geometry > GRT_GEOM_KERR_BL) return fail(-EINVAL, "unknown geometry");
+  if (d->geometry < GRT_GEOM_EUCLIDEAN || d->geometry > GRT_GEOM_EUCLIDEAN_SPHERICAL)
+    return fail(-EINVAL, "unknown geometry");
   if (d->n_objects > GRT_MAX_OBJECTS) return fail(-EINVAL, "too many objects");
   auto check_tex = [&](const grt_texture_desc& t) -> int {
     if (t.kind == GRT_TEX_BITMAP && (!t.rgba || !t.width || !t.height)) return fail(-EINVAL, "bitmap texture without texels");

@@ -319,6 +319,19 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
            a * r * (v_theta * v_theta + v_phi * v_phi * st * st);
     o[6] = -(two_over_r)*v_r * v_theta + st * ct * v_phi * v_phi;
     o[7] = -(two_over_r)*v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
+  } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:48-70
+    double r = y[1], theta = y[2];
+    double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
+    double st, ct;
+    rsincos(theta, &st, &ct);
+    o[0] = v_t;
+    o[1] = v_r;
+    o[2] = v_theta;
+    o[3] = v_phi;
+    o[4] = 0.0;
+    o[5] = r * (v_theta * v_theta + v_phi * v_phi * st * st);
+    o[6] = -(2.0 / r) * v_r * v_theta + st * ct * v_phi * v_phi;
+    o[7] = -(2.0 / r) * v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
   } else if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:141-174
     double radius = S.radius, a = S.a, e = rc.e, l_z = rc.lz, q = rc.q;
     double r = y[1], theta = y[2];
@@ -440,7 +453,7 @@ GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, 
 // Cartesian spatial position of a state (scene.rs:48-69 get_position / point.rs:125-154).
 template <int G>
 GDEV void to_cart(const DevScene& S, const double* y, double* c) {
-  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     double st, ct, sp, cp;
     rsincos(y[2], &st, &ct);
     rsincos(y[3], &sp, &cp);
@@ -525,6 +538,9 @@ GDEV double inner(const DevScene& S, const double* pos, double st, double ct, co
     double r = pos[1];
     double a = 1.0 - S.radius / r;
     return a * v[0] * w[0] - v[1] * w[1] / a - r * r * v[2] * w[2] - r * r * st * st * v[3] * w[3];
+  } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:80-91
+    double r = pos[1];
+    return 1.0 * v[0] * w[0] - v[1] * w[1] - r * r * v[2] * w[2] - r * r * st * st * v[3] * w[3];
   } else if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:338-359
     double g[4][4];
     metric_bl(S.radius, S.a, pos[1], st, ct, g);
@@ -851,7 +867,7 @@ GDEV int should_stop(const DevScene& S, const double* y, double* c, bool& c_vali
   // [|r|, |r| + far_a] in the curvilinear charts, so away from the celestial shell the
   // answer follows from r and the conversion is skipped.
   bool escaped = false, decided = false;
-  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     if (!c_valid && S.far_ok) {
       double ar = fabs(y[1]), hi = ar + S.far_a;
       if (hi * hi < S.cel_lo2) decided = true;
@@ -882,7 +898,7 @@ GDEV int should_stop(const DevScene& S, const double* y, double* c, bool& c_vali
 //    (1e-9 margins) keeps both ends strictly outside.
 template <int G>
 GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
-  if constexpr (G != GRT_GEOM_SCHWARZSCHILD && G != GRT_GEOM_KERR_BL) {
+  if constexpr (G != GRT_GEOM_SCHWARZSCHILD && G != GRT_GEOM_KERR_BL && G != GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     return false;
   } else {
     if (!S.far_ok) return false;
@@ -1207,6 +1223,10 @@ hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const Traj
     case GRT_GEOM_KERR_BL:
       hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, tl);
       break;
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL:
+      hipLaunchKernelGGL(trajectory_kernel<GRT_GEOM_EUCLIDEAN_SPHERICAL>, dim3(blocks), dim3(64), 0, stream, d_scene,
+                         tl);
+      break;
     default:
       return hipErrorInvalidValue;
   }
@@ -1275,6 +1295,10 @@ hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& w
       hipLaunchKernelGGL(probe_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n_tiles,
                          cap, d_steps);
       break;
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL:
+      hipLaunchKernelGGL(probe_kernel<GRT_GEOM_EUCLIDEAN_SPHERICAL>, dim3(blocks), dim3(64), 0, stream, d_scene, wl,
+                         n_tiles, cap, d_steps);
+      break;
     default:
       return hipErrorInvalidValue;
   }
@@ -1312,9 +1336,9 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
   double x[4];  // step.x = intersection point converted to the native chart
   double st = 0.0, ct = 0.0;
   x[0] = 0.0;
-  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     cart_to_sph(wx, wy, wz, &x[1], &x[2], &x[3]);
-    st = rsin(x[2]);  // the only trig of schwarzschild.rs:90-102 (ct unused)
+    st = rsin(x[2]);  // the only trig of the spherical inner products (ct unused)
   } else if constexpr (G == GRT_GEOM_KERR_BL) {
     cart_to_bl(S.a, wx, wy, wz, &x[1], &x[2], &x[3]);
     rsincos(x[2], &st, &ct);
@@ -1325,7 +1349,7 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
   }
   double u[4];
   if (o.kind == GRT_OBJ_DISC) {  // disc.rs:101-110: circular-orbit emitter
-    if constexpr (G == GRT_GEOM_EUCLIDEAN) {
+    if constexpr (G == GRT_GEOM_EUCLIDEAN || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // at rest in flat space
       u[0] = 1.0; u[1] = 0.0; u[2] = 0.0; u[3] = 0.0;
     } else {
       double r;
@@ -1438,10 +1462,10 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     for (int k = 0; k < 8; ++k) y[k] = ws.y[k * n + idx];
     double th, ph;  // get_as_spherical (point.rs:172-188)
     double st = 0.0, ct = 0.0;
-    if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL) {
+    if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
       th = rem_euclid(y[2], PI);
       ph = rem_euclid(y[3] + PI, TWO_PI) - PI;
-      if constexpr (G == GRT_GEOM_SCHWARZSCHILD) st = rsin(y[2]);  // inner_product: sin only
+      if constexpr (G != GRT_GEOM_KERR_BL) st = rsin(y[2]);  // inner_product: sin only
       else rsincos(y[2], &st, &ct);
     } else {
       double rr;
@@ -1494,6 +1518,9 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
       return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
     case GRT_GEOM_KERR_BL:
       return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL:
+      return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads,
+                                                    stream);
     default:
       return hipErrorInvalidValue;
   }

@@ -233,6 +233,8 @@ static int load_geometry(const char* toml_path, const grt_global_opts* opts, Tom
   if (!variant(get(root, "geometry_type"), gname, &gb)) return fail("missing or invalid `geometry_type`");
   if (gname == "Euclidean") {
     d.geometry = GRT_GEOM_EUCLIDEAN;
+  } else if (gname == "EuclideanSpherical") {
+    d.geometry = GRT_GEOM_EUCLIDEAN_SPHERICAL;
   } else if (gname == "Schwarzschild") {
     d.geometry = GRT_GEOM_SCHWARZSCHILD;
     if (!num(*gb, "radius", &d.radius, err) || !num(*gb, "horizon_epsilon", &d.horizon_epsilon, err)) return fail(err);
@@ -242,7 +244,7 @@ static int load_geometry(const char* toml_path, const grt_global_opts* opts, Tom
         !num(*gb, "horizon_epsilon", &d.horizon_epsilon, err))
       return fail(err);
   } else {
-    return fail("geometry `" + gname + "` is out of scope (Euclidean, Schwarzschild, Kerr, KerrBL supported)");
+    return fail("unknown geometry `" + gname + "`");
   }
   d.max_steps = opts->max_steps;
   d.max_radius = opts->max_radius;
@@ -314,7 +316,8 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
   // camera position in the geometry's native chart (cli/<geometry>.rs)
   double cart[4] = {0.0, opts->camera_position[0], opts->camera_position[1], opts->camera_position[2]};
   double pos[4];
-  if (d.geometry == GRT_GEOM_SCHWARZSCHILD) grt_cartesian_to_spherical(cart, pos);
+  if (d.geometry == GRT_GEOM_SCHWARZSCHILD || d.geometry == GRT_GEOM_EUCLIDEAN_SPHERICAL)
+    grt_cartesian_to_spherical(cart, pos);
   else if (d.geometry == GRT_GEOM_KERR_BL) grt_cartesian_to_boyer_lindquist(d.a, cart, pos);
   else std::memcpy(pos, cart, sizeof(pos));
 
@@ -378,7 +381,7 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
         return fail("Disc: " + err);
       // geometry.get_temperature_computer (euclidean.rs:219-226, schwarzschild.rs:267-279,
       // kerr.rs:498-510, kerr_bl.rs:412-424)
-      if (d.geometry == GRT_GEOM_EUCLIDEAN) {
+      if (d.geometry == GRT_GEOM_EUCLIDEAN || d.geometry == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
         o.temp_kind = GRT_TEMP_CONSTANT;
         o.temp_constant = temperature;
       } else {

@@ -142,6 +142,11 @@ static double inner_product(const Geo& g, const V4& pos, const V4& v, const V4& 
       return a * v[0] * w[0] - v[1] * w[1] / a - r * r * v[2] * w[2] -
              r * r * std::sin(theta) * std::sin(theta) * v[3] * w[3];
     }
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL: {  // euclidean_spherical.rs:80-91
+      double r = pos[1], theta = pos[2];
+      return 1.0 * v[0] * w[0] - v[1] * w[1] - r * r * v[2] * w[2] -
+             r * r * std::sin(theta) * std::sin(theta) * v[3] * w[3];
+    }
     case GRT_GEOM_KERR: {
       M4 m;
       ks_metric(g.radius, g.a, pos[1], pos[2], pos[3], m);
@@ -197,6 +202,7 @@ static V4 stationary_velocity(const Geo& g, const V4& p) {
   V4 u{{0, 0, 0, 0}};
   switch (g.kind) {
     case GRT_GEOM_EUCLIDEAN:
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL:  // euclidean_spherical.rs:168-170
       u[0] = 1.0;
       break;
     case GRT_GEOM_SCHWARZSCHILD: {
@@ -222,7 +228,8 @@ static V4 stationary_velocity(const Geo& g, const V4& p) {
 }
 
 static V4 zamo_velocity(const Geo& g, const V4& p) {
-  if (g.kind == GRT_GEOM_EUCLIDEAN || g.kind == GRT_GEOM_SCHWARZSCHILD) return stationary_velocity(g, p);
+  if (g.kind == GRT_GEOM_EUCLIDEAN || g.kind == GRT_GEOM_SCHWARZSCHILD || g.kind == GRT_GEOM_EUCLIDEAN_SPHERICAL)
+    return stationary_velocity(g, p);
   if (g.kind == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:373-382
     double ut, uphi;
     zamo_killing(g.radius, g.a, p[1], p[2], &ut, &uphi);
@@ -280,6 +287,14 @@ static Tetrad get_tetrad_at(const Geo& g, const V4& p) {
       T.x = e_phi;
       T.y = neg(e_theta);
       T.z = neg(e_r);
+      break;
+    }
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL: {  // euclidean_spherical.rs:100-112
+      double r = p[1], theta = p[2];
+      T.t = V4{{1.0, 0.0, 0.0, 0.0}};
+      T.x = V4{{0.0, 0.0, 0.0, 1.0 / (r * std::sin(theta))}};
+      T.y = neg(V4{{0.0, 0.0, 1.0 / r, 0.0}});
+      T.z = neg(V4{{0.0, 1.0, 0.0, 0.0}});
       break;
     }
     case GRT_GEOM_SCHWARZSCHILD: {  // schwarzschild.rs:116-132
@@ -346,6 +361,10 @@ static void lorentz_transformation(const Geo& g, const V4& pos, const V4& vel, M
         }
       break;
     }
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL:  // euclidean_spherical.rs:114-122: identity
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) L[i][j] = (i == j) ? 1.0 : 0.0;
+      break;
     case GRT_GEOM_SCHWARZSCHILD: {  // schwarzschild.rs:134-179
       double r = pos[1], theta = pos[2];
       double a = 1.0 - g.radius / r;
@@ -410,7 +429,7 @@ static void spatial_cartesian(const Geo& g, const V4& pos, const V4& v, double o
   }
   double r = pos[1], theta = rem_euclid(pos[2], PI), phi = rem_euclid(pos[3] + PI, 2.0 * PI) - PI;
   double dr = v[1], dtheta = v[2], dphi = v[3];
-  if (g.kind == GRT_GEOM_SCHWARZSCHILD) {
+  if (g.kind == GRT_GEOM_SCHWARZSCHILD || g.kind == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     double st = std::sin(theta), ct = std::cos(theta), sp = std::sin(phi), cp = std::cos(phi);
     out[0] = st * cp * dr + r * ct * cp * dtheta - r * st * sp * dphi;
     out[1] = st * sp * dr + r * ct * sp * dtheta + r * st * cp * dphi;
@@ -433,7 +452,9 @@ static double spatial_handedness(const Geo& g, const V4& pos, const Tetrad& T) {
   double c2 = y[0] * z[1] - y[1] * z[0];
   double triple = x[0] * c0 + x[1] * c1 + x[2] * c2;
   if (!std::isfinite(triple) || std::fabs(triple) <= 1e-12)
-    return (g.kind == GRT_GEOM_SCHWARZSCHILD || g.kind == GRT_GEOM_KERR_BL) ? -1.0 : 1.0;
+    return (g.kind == GRT_GEOM_SCHWARZSCHILD || g.kind == GRT_GEOM_KERR_BL || g.kind == GRT_GEOM_EUCLIDEAN_SPHERICAL)
+               ? -1.0
+               : 1.0;
   return triple >= 0.0 ? 1.0 : -1.0;
 }
 
@@ -511,6 +532,31 @@ int ray_at(int geometry, double radius, double a, const double position[3], cons
       }
       pos = cart;
       mom = V4{{spatial_norm, d1, d2, d3}};
+      break;
+    }
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL: {  // cli/euclidean_spherical.rs:77-142
+      pos = cart_to_sph_v(cart);
+      const double r = pos[1], theta = pos[2], phi = pos[3];
+      if (!(std::isfinite(r) && r > 0.0)) {
+        err = "Euclidean-spherical render_ray_at requires r > 0, got r=" + rust_display_f64(r) + ".";
+        return -EINVAL;
+      }
+      const double sin_theta = std::sin(theta);
+      if (!(std::isfinite(sin_theta) && std::fabs(sin_theta) > 1e-12)) {
+        err = "Euclidean-spherical render_ray_at is undefined on the polar axis (theta=" + rust_display_f64(theta) +
+              ").";
+        return -EINVAL;
+      }
+      const double spatial_norm = std::sqrt(d1 * d1 + d2 * d2 + d3 * d3);
+      if (!(std::isfinite(spatial_norm) && spatial_norm > 0.0)) {
+        err = "render_ray_at direction must have a non-zero finite spatial part.";
+        return -EINVAL;
+      }
+      const double r_dot = sin_theta * std::cos(phi) * d1 + sin_theta * std::sin(phi) * d2 + std::cos(theta) * d3;
+      const double theta_unit_dot =
+          std::cos(theta) * std::cos(phi) * d1 + std::cos(theta) * std::sin(phi) * d2 - sin_theta * d3;
+      const double phi_unit_dot = -std::sin(phi) * d1 + std::cos(phi) * d2;
+      mom = V4{{spatial_norm, r_dot, theta_unit_dot / r, phi_unit_dot / (r * sin_theta)}};
       break;
     }
     case GRT_GEOM_SCHWARZSCHILD: {  // cli/schwarzschild.rs:89-121

@@ -48,7 +48,7 @@ std::string rust_display_f64(double v) {
 static void to_cartesian(int geometry, double a, const double* x, double* c) {
   const double t = x[0], r = x[1], theta = x[2], phi = x[3];
   c[0] = t;
-  if (geometry == GRT_GEOM_SCHWARZSCHILD) {
+  if (geometry == GRT_GEOM_SCHWARZSCHILD || geometry == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     c[1] = r * std::sin(theta) * std::cos(phi);
     c[2] = r * std::sin(theta) * std::sin(phi);
     c[3] = r * std::cos(theta);

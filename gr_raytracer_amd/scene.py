@@ -444,7 +444,8 @@ class SceneBuilder:
         """Disc with geometry.get_temperature_computer(temperature, inner, outer)."""
         o = self.d.objects[self.d.n_objects]
         o.kind, o.inner_radius, o.outer_radius = L.OBJ_DISC, inner_radius, outer_radius
-        const = self.d.geometry == L.GEOM_EUCLIDEAN if constant_temperature is None else constant_temperature
+        const = (self.d.geometry in (L.GEOM_EUCLIDEAN, L.GEOM_EUCLIDEAN_SPHERICAL) if constant_temperature is None
+                 else constant_temperature)
         if const:
             o.temp_kind, o.temp_constant = L.TEMP_CONSTANT, temperature
         else:

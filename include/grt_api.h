@@ -36,12 +36,14 @@ extern "C" {
 
 /* ---- enums (values are part of the ABI) -------------------------------------- */
 
-/* configuration.rs:111-129 GeometryType (EuclideanSpherical is out of scope). */
+/* configuration.rs:111-129 GeometryType. */
 enum grt_geometry_kind {
   GRT_GEOM_EUCLIDEAN = 0,     /* geometry/euclidean.rs, Cartesian chart, (+,-,-,-)   */
   GRT_GEOM_SCHWARZSCHILD = 1, /* geometry/schwarzschild.rs, spherical chart, (+,-,-,-) */
   GRT_GEOM_KERR = 2,          /* geometry/kerr.rs, Kerr-Schild Cartesian, (-,+,+,+)   */
-  GRT_GEOM_KERR_BL = 3        /* geometry/kerr_bl.rs, Boyer-Lindquist, (-,+,+,+)      */
+  GRT_GEOM_KERR_BL = 3,       /* geometry/kerr_bl.rs, Boyer-Lindquist, (-,+,+,+)      */
+  GRT_GEOM_EUCLIDEAN_SPHERICAL = 4 /* geometry/euclidean_spherical.rs, flat space in the
+                                      spherical chart, (+,-,-,-)                        */
 };
 
 /* configuration.rs:162-177 TextureConfig. */

@@ -10,7 +10,8 @@
 //   * Scene::color_of_ray, get_uv_coordinates   src/rendering/scene.rs:114-231
 //   * Objects::intersects, step_at_intersection src/scene_objects/objects.rs:27-120
 //   * Disc / Sphere intersections + emitters    src/scene_objects/{disc,sphere}.rs
-//   * Schwarzschild / Kerr / KerrBL / Euclidean src/geometry/*.rs (RHS, metrics, stops)
+//   * Schwarzschild / Kerr / KerrBL / Euclidean / EuclideanSpherical
+//                                               src/geometry/*.rs (RHS, metrics, stops)
 //   * redshift, textures, temperature lookup    src/rendering/{redshift,texture,temperature}.rs
 //   * camera ray generation                     src/rendering/camera.rs:214-254
 //   * frame driver + adaptive supersampling     src/rendering/raytracer.rs:91-458
@@ -411,6 +412,50 @@ struct Schwarzschild : Geometry {
     Err e = killing_coefficients(radius, 0.0, radial_coordinate(p), &c);
     if (e != OK) return e;
     *out = FourVector{CS::Spherical, {c.u_t, 0.0, 0.0, c.u_phi}};
+    return OK;
+  }
+};
+
+// ---- EuclideanSpherical: flat space in the spherical chart (geometry/euclidean_spherical.rs) ----
+struct EuclideanSphericalSolver : GeodesicSolver {
+  void apply(const double* y, double* o) const override {  // :48-70
+    double r = y[1], theta = y[2];
+    double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
+    double st, ct;
+    rhs_sincos(theta, &st, &ct);
+    double a_t = 0.0;
+    double a_r = r * (v_theta * v_theta + v_phi * v_phi * st * st);
+    double a_theta = -(2.0 / r) * v_r * v_theta + st * ct * v_phi * v_phi;
+    double a_phi = -(2.0 / r) * v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
+    o[0] = v_t; o[1] = v_r; o[2] = v_theta; o[3] = v_phi;
+    o[4] = a_t; o[5] = a_r; o[6] = a_theta; o[7] = a_phi;
+  }
+  FourVector momentum_from_state(const double* y) const override {
+    return FourVector{CS::Spherical, {y[4], y[5], y[6], y[7]}};
+  }
+};
+struct EuclideanSpherical : Geometry {
+  CS cs() const override { return CS::Spherical; }
+  double signature0() const override { return 1.0; }
+  double inner_product(const Point& p, const FourVector& v, const FourVector& w) const override {
+    double r = p[1], theta = p[2];  // :80-91
+    return 1.0 * v[0] * w[0] - v[1] * w[1] - r * r * v[2] * w[2] -
+           r * r * g_sin(theta) * g_sin(theta) * v[3] * w[3];
+  }
+  bool inside_horizon(const Point&) const override { return false; }                  // :124-126
+  bool closed_orbit(const Point&, uint64_t, uint64_t) const override { return false; }  // :128-130
+  std::unique_ptr<GeodesicSolver> solver(const Ray&) const override {
+    return std::unique_ptr<GeodesicSolver>(new EuclideanSphericalSolver());
+  }
+  double radial_coordinate(const Point& p) const override {  // :136-146
+    if (p.cs == CS::Cartesian) return get_as_spherical(p).x;
+    return p[1];
+  }
+  FourVector stationary_velocity(const Point&) const override {  // :168-170
+    return FourVector{CS::Spherical, {1.0, 0.0, 0.0, 0.0}};
+  }
+  Err circular_orbit_velocity(const Point&, FourVector* out) const override {  // :177-183
+    *out = FourVector{CS::Spherical, {1.0, 0.0, 0.0, 0.0}};
     return OK;
   }
 };
@@ -1220,6 +1265,7 @@ static void init_ctx(SceneCtx& S, const grt_scene_desc* d) {
     case GRT_GEOM_EUCLIDEAN: S.g.reset(new Euclidean()); break;
     case GRT_GEOM_SCHWARZSCHILD: S.g.reset(new Schwarzschild()); break;
     case GRT_GEOM_KERR: S.g.reset(new Kerr()); break;
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL: S.g.reset(new EuclideanSpherical()); break;
     default: S.g.reset(new KerrBL()); break;
   }
   S.g->radius = d->radius;

@@ -133,6 +133,13 @@ def test_c1_euclidean_full_frame(grt, oracle, gpu):
     compare_rect(grt, oracle, hs, (0, 0, 256, 256))
 
 
+def test_euclidean_spherical_frame(grt, oracle, gpu):
+    """scene-definitions/euclidean-spherical.toml (flat space in the spherical chart,
+    SURVEY.md 8(f) row 4) at the CLI's default camera, 160 x 128."""
+    hs = host_scene(grt, "euclidean-spherical.toml", c1_opts(grt, width=160, height=128))
+    compare_rect(grt, oracle, hs, (0, 0, 128, 160))
+
+
 @pytest.mark.parametrize("rect", [(718, 718, 64, 64), (1000, 600, 32, 32), (0, 0, 24, 40), (1492, 1490, 8, 10)])
 def test_c2_schwarzschild_crops(grt, oracle, gpu, rect):
     """configs[1]: shadow centre, disc edge, corner and ragged bottom-right crops."""

@@ -9,9 +9,10 @@ import pytest
 from conftest import RESOURCES, SCENES, c1_opts, c2_opts, c3_opts, c4_opts, host_scene
 
 SCENE_OPTS = {"euclidean.toml": c1_opts, "schwarzschild.toml": c2_opts, "schwarzschild-sphere.toml": c2_opts,
-              "kerr.toml": c4_opts, "kerr-sphere.toml": c4_opts, "kerr-bl.toml": c3_opts}
+              "kerr.toml": c4_opts, "kerr-sphere.toml": c4_opts, "kerr-bl.toml": c3_opts,
+              "euclidean-spherical.toml": c1_opts}
 GEOMETRY = {"euclidean.toml": 0, "schwarzschild.toml": 1, "schwarzschild-sphere.toml": 1, "kerr.toml": 2,
-            "kerr-sphere.toml": 2, "kerr-bl.toml": 3}
+            "kerr-sphere.toml": 2, "kerr-bl.toml": 3, "euclidean-spherical.toml": 4}
 
 
 @pytest.mark.parametrize("name", sorted(SCENE_OPTS))
@@ -35,7 +36,8 @@ def _minkowski_check(oracle, d):
     assert np.sign(g[0, 0]) == -np.sign(g[1, 1]) == -np.sign(g[2, 2]) == -np.sign(g[3, 3])
 
 
-@pytest.mark.parametrize("name", ["schwarzschild.toml", "kerr.toml", "kerr-bl.toml", "euclidean.toml"])
+@pytest.mark.parametrize("name", ["schwarzschild.toml", "kerr.toml", "kerr-bl.toml", "euclidean.toml",
+                                  "euclidean-spherical.toml"])
 def test_camera_tetrads_are_orthonormal(grt, oracle, name):
     hs = host_scene(grt, name, SCENE_OPTS[name](grt))
     _minkowski_check(oracle, hs.desc)

@@ -123,6 +123,10 @@ KAT_SCENES = {
         lambda g: kat_scene(g, 1, 1.0, ((0.0, 10.0, PI / 2, PI), (-1.0 / math.sqrt(1 - 0.1), 0.0, 0.0, 0.0),
                                         PI / 2, 11, 11, PI / 2, 0.0, PI / 2), 0.5, 3.0, 4.0),
         (5, 5), (0.0, 0.0, 0.0, 1.0), 1),  # :604-633
+    "hits_sphere_spherical": (  # EuclideanSpherical, camera on the -z axis (theta = pi)
+        lambda g: kat_scene(g, 4, 0.0, (tuple(g.cartesian_to_spherical((0.0, 0.0, 0.0, -10.0))), (1.0, 0, 0, 0),
+                                        PI / 2, 11, 11), 2.0, 0.2, 0.3),
+        (5, 5), (0.052562486896837575, 0.0271025410675224, 0.002463867369774764, 1.0), None),  # :440-478
     "intersects_with_disk": (
         lambda g: kat_scene(g, 0, 0.0, ((0.0, 7.0, 0.0, 0.8), (1.0, 0, 0, 0), PI / 4, 101, 101), 1.0, 2.0, 7.0),
         (0, 51), (0.022994536463607135, 0.009197814585442854, 0.12110455021248553, 1.0), None),  # :635-666

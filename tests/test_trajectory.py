@@ -85,7 +85,8 @@ def test_csv_writer(grt, tmp_path, geometry):
         assert np.allclose(got, want, rtol=1e-14, atol=1e-300), (got, want)
 
 
-@pytest.mark.parametrize("geometry,radius,a", [(0, 0.0, 0.0), (1, 1.0, 0.0), (2, 1.0, 0.5), (3, 1.0, 0.5)])
+@pytest.mark.parametrize("geometry,radius,a", [(0, 0.0, 0.0), (1, 1.0, 0.0), (2, 1.0, 0.5), (3, 1.0, 0.5),
+                                               (4, 0.0, 0.0)])
 def test_ray_at_momentum_norm(grt, oracle, geometry, radius, a):
     for position, direction in [((0.0, 4.0, -18.0), (0.0, 1.0, 0.0)), ((18.0, 0.0, 0.0), (-1.0, 0.0, 0.0)),
                                 ((-10.0, 3.0, 2.5), (0.3, -0.2, 0.9))]:
@@ -97,6 +98,9 @@ def test_ray_at_momentum_norm(grt, oracle, geometry, radius, a):
         # (cli/schwarzschild.rs:100-112): g(p, p) = 1 - |d|^2 in the local frame
         want = 1.0 - float(np.dot(direction, direction)) if geometry == 1 else 0.0
         assert abs(n - want) <= 1e-12 * scale * scale, (geometry, n, want)
+        if geometry == 4:  # cli/euclidean_spherical.rs: p^t = |d|, null for any |d|
+            want = 0.0
+            assert abs(n) <= 1e-12 * scale * scale, (geometry, n)
         if geometry == 0:  # cli/euclidean.rs:90-91: (|d|, d) at (0, position)
             d = np.array(direction)
             assert np.array_equal(mom, [math.sqrt(d @ d), *d]) and np.array_equal(pos, [0.0, *position])
@@ -153,6 +157,7 @@ CASES = {
     "C2": ("schwarzschild.toml", c2_opts, [(750, 750), (740, 760), (0, 0), (700, 1499), (770, 745)]),
     "C3": ("kerr-bl.toml", c3_opts, [(750, 750), (760, 700), (100, 100)]),
     "C4": ("kerr.toml", c4_opts, [(100, 100), (2048, 600), (3000, 3900)]),
+    "ES": ("euclidean-spherical.toml", c1_opts, [(128, 128), (10, 200), (200, 40)]),
 }
 
 
@@ -185,6 +190,7 @@ RAY_AT = [  # the reference's render_ray_at tests (cli/*.rs) plus longer rays
     (3, 1.0, 0.5, (18.0, 0.0, 0.0), (1.0, 0.0, 0.0)),
     (1, 1.0, 0.0, (-12.0, 1.0, 0.5), (1.0, 0.05, 0.0)),
     (3, 1.0, 0.499, (-10.0, 0.0, -0.5), (1.0, 0.1, 0.05)),
+    (4, 0.0, 0.0, (0.0, 4.0, -18.0), (0.0, 1.0, 0.0)),  # EuclideanSpherical (cli/euclidean_spherical.rs)
 ]
 
 
@@ -208,13 +214,14 @@ def test_trace_rays_matches_oracle_integrator(grt, oracle, gpu, max_steps, max_r
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,lines_expected", [(0, None), (1, 12), (2, 12), (3, None)])
+@pytest.mark.parametrize("k,lines_expected", [(0, None), (1, 12), (2, 12), (3, None), (6, None)])
 def test_cli_render_ray_at_reference_tests(grt, oracle, gpu, tmp_path, k, lines_expected):
     """cli/{schwarzschild,kerr,kerr_bl}.rs test_render_*_ray_at: max_steps 10, max_radius
     20 -> "i,t,tau,x,y,z" + 10 records + the trailing newline = 12 split lines (KerrBL's
     test checks the header only).  Every case: as many records as the oracle's run."""
     geometry, radius, a, position, direction = RAY_AT[k]
-    toml = {0: "euclidean.toml", 1: "schwarzschild.toml", 2: "kerr.toml", 3: "kerr-bl.toml"}[geometry]
+    toml = {0: "euclidean.toml", 1: "schwarzschild.toml", 2: "kerr.toml", 3: "kerr-bl.toml",
+            4: "euclidean-spherical.toml"}[geometry]
     text = (SCENES / toml).read_text()  # the tests' geometry: a = 0.5, horizon_epsilon = 1e-5
     text = re.sub(r"^a\s*=.*$", f"a = {a}", text, flags=re.M)
     text = re.sub(r"^horizon_epsilon\s*=.*$", "horizon_epsilon = 1e-5", text, flags=re.M)
