@@ -196,6 +196,14 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     std::frexp(d.radius, &ex);
     ds.div_share = (std::fpclassify(d.radius) == FP_NORMAL && ex > -500 && ex < 500) ? 1 : 0;
   }
+  {  // exact controller shortcuts (geodesic.hip step_control); off unless epsilon is a moderate normal
+    int ex = 0;
+    std::frexp(d.epsilon, &ex);
+    const bool ok = std::fpclassify(d.epsilon) == FP_NORMAL && d.epsilon > 0.0 && ex > -900 && ex < 900;
+    ds.pow_skip_err = ok ? d.epsilon / 1800.0 * (1.0 - 1e-9) : 0.0;
+    ds.small_lo = ok ? d.epsilon * 1e-5 * (1.0 - 1e-9) : 0.0;
+    ds.small_hi = ok ? d.epsilon * 1e-5 * (1.0 + 1e-9) : HUGE_VAL;
+  }
   const grt_camera_desc& c = d.camera;
   for (int k = 0; k < 4; ++k) {
     ds.cam.pos[k] = c.position[k];

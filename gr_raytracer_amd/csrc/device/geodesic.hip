@@ -931,8 +931,10 @@ GDEV int step_control(const DevScene& S, double err, double& h_cur, int& retries
   // h_prop = err > 0 ? BETA*h*(eps/err)^(1/5) : 4h, then min(., 4h).  For eps/err >= 1800,
   // BETA*1800^(1/5) = 4.0308 > 4, so the min is 4h whatever pow's last ulp: pow is
   // skipped there (the far-field steps), which leaves every result bit-identical.
+  // err < pow_skip_err (host: eps/1800 * (1 - 1e-9)) proves eps/err > 1800: the division
+  // is skipped with the pow.
   double h_prop = h_cur * H_GROWTH;
-  if (err > 0.0) {
+  if (err > 0.0 && !(err < S.pow_skip_err)) {
     const double ratio = S.epsilon / err;
     if (ratio < POW_SATURATED) h_prop = BETA * h_cur * rpow(ratio, INV_ORDER);
   }
@@ -945,7 +947,9 @@ GDEV int step_control(const DevScene& S, double err, double& h_cur, int& retries
     h_cur = rclamp(h_prop / 2.0, H_MIN, H_MAX);
     return (++retries >= MAX_RETRY) ? STEP_FAILED : STEP_RETRY;
   }
-  h_next = (err / S.epsilon < SMALL_ERR) ? rclamp(h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
+  // err / eps < 1e-5, decided without the division away from the threshold (1e-9 margins)
+  const bool small = err < S.small_lo || (!(err > S.small_hi) && err / S.epsilon < SMALL_ERR);
+  h_next = small ? rclamp(h_cur * H_GROWTH, H_MIN, H_MAX) : h_prop;
   return STEP_ACCEPTED;
 }
 
