@@ -203,6 +203,8 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     ds.pow_skip_err = ok ? d.epsilon / 1800.0 * (1.0 - 1e-9) : 0.0;
     ds.small_lo = ok ? d.epsilon * 1e-5 * (1.0 - 1e-9) : 0.0;
     ds.small_hi = ok ? d.epsilon * 1e-5 * (1.0 + 1e-9) : HUGE_VAL;
+    const double t = std::fmin(ds.pow_skip_err, ds.small_lo);
+    ds.tiny_err_sq = (ok && t >= 1e-150) ? t * t * (1.0 - 1e-9) : 0.0;  // t^2 stays a normal
   }
   const grt_camera_desc& c = d.camera;
   for (int k = 0; k < 4; ++k) {

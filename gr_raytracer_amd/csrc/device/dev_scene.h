@@ -64,7 +64,7 @@ struct DevScene {
   int32_t div_share;      // radius is a moderate normal: x / r divisions may share 1 / r
   // step controller thresholds (host, 1e-9 margins): err below pow_skip_err proves
   // eps/err > 1800; err below small_lo / above small_hi decides err/eps < 1e-5
-  double pow_skip_err, small_lo, small_hi;
+  double pow_skip_err, small_lo, small_hi, tiny_err_sq;
   double far_a, cel_lo2, cel_hi2;
   DevCamera cam;
   DevTexture celestial;

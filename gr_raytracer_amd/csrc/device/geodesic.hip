@@ -387,7 +387,8 @@ struct Dim {
   static constexpr int D = (G == GRT_GEOM_KERR_BL) ? 6 : 8;
 };
 
-// One rkf45_step (runge_kutta.rs:86-125).  Returns the truncation error norm.
+// One rkf45_step (runge_kutta.rs:86-125).  Returns the SQUARED truncation error norm:
+// the controller takes the (correctly rounded) sqrt only when the decision needs it.
 template <int G>
 GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
                         double* yn) {
@@ -446,7 +447,7 @@ GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, 
     res += e[2] * e[2];
     res += e[3] * e[3];
   }
-  return sqrt(res);
+  return res;
 }
 
 // ---- chart helpers ----
@@ -927,7 +928,15 @@ GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
 // h_cur is the retry's step (STEP_RETRY), or the 100th retry failed (STEP_FAILED,
 // Err(MaxStepsReached)).
 enum { STEP_ACCEPTED = 0, STEP_RETRY = 1, STEP_FAILED = 2 };
-GDEV int step_control(const DevScene& S, double err, double& h_cur, int& retries, double& h_next) {
+GDEV int step_control(const DevScene& S, double err_sq, double& h_cur, int& retries, double& h_next) {
+  // err_sq < tiny_err_sq (host: min(pow_skip_err, small_lo)^2 * (1 - 1e-9)) proves
+  // err = sqrt(err_sq) < both thresholds (and < eps): accepted with h_next = clamp(4h),
+  // the outcome of every branch below, without the sqrt (the far-field steps)
+  if (err_sq < S.tiny_err_sq) {
+    h_next = rclamp(h_cur * H_GROWTH, H_MIN, H_MAX);
+    return STEP_ACCEPTED;
+  }
+  const double err = sqrt(err_sq);
   // h_prop = err > 0 ? BETA*h*(eps/err)^(1/5) : 4h, then min(., 4h).  For eps/err >= 1800,
   // BETA*1800^(1/5) = 4.0308 > 4, so the min is 4h whatever pow's last ulp: pow is
   // skipped there (the far-field steps), which leaves every result bit-identical.
@@ -1065,10 +1074,10 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
 
     // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
     double yn[8];
-    double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
+    const double err_sq = rkf_attempt<G>(S, rc, y, h_cur, yn);
     n_att++;
     double h_next;
-    const int ctl = step_control(S, err, h_cur, retries, h_next);
+    const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
     if (ctl != STEP_ACCEPTED) {
       if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
         store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
@@ -1189,8 +1198,8 @@ __global__ void __launch_bounds__(64) trajectory_kernel(const DevScene* __restri
     double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
     int retries = 0, ctl;
     do {
-      const double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
-      ctl = step_control(S, err, h_cur, retries, h_next);
+      const double err_sq = rkf_attempt<G>(S, rc, y, h_cur, yn);
+      ctl = step_control(S, err_sq, h_cur, retries, h_next);
     } while (ctl == STEP_RETRY);
     if (ctl == STEP_FAILED) {
       status = GRT_ERR_MAX_STEPS_REACHED;
@@ -1264,8 +1273,8 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
     double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
     int retries = 0, ctl;
     do {
-      const double err = rkf_attempt<G>(S, rc, y, h_cur, yn);
-      ctl = step_control(S, err, h_cur, retries, h_next);
+      const double err_sq = rkf_attempt<G>(S, rc, y, h_cur, yn);
+      ctl = step_control(S, err_sq, h_cur, retries, h_next);
     } while (ctl == STEP_RETRY);
     if (ctl == STEP_FAILED) break;
     h = h_next;
