@@ -1,4 +1,3 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
-for m in 1 0; do GRT_SCHEDULE=$m timeout -k 10 120 python3 tools/prof_target.py c3 || exit 1; done
-bash tools/gpu_round.sh r01b
+for v in pre cur pre cur; do GRT_LIB=variants/$v/libgrt.so GRT_LIB_ALLOW_MISSING=1 timeout -k 10 300 python3 tools/c4_shard_time.py 8 0 | sed "s/^/$v /" || exit 1; done
