@@ -141,6 +141,60 @@ GRT_GLIBC_FN bool pow_fast(double x, double y, double* out) {
   return true;
 }
 
+// ---------------------------------------------------------------------- exp ----
+// glibc 2.35 __exp_fma (sysdeps/ieee754/dbl-64/e_exp.c, ARM optimized routines, the
+// FMA ifunc build): x = k ln2/128 + r, exp(x) = 2^(k/128) exp(r) with the same
+// __exp_data table and polynomial as pow's exp_inline above.  Every fma_() below is
+// one vfmadd of the disassembled __exp_fma; specialcase() follows its k > 0 (scale
+// 2^1009) and k < 0 (subnormal rounding) branches.  Defined for every input
+// (tests/test_glibc_math.py checks it against glibc exp, bit for bit).
+GRT_GLIBC_FN double exp_special(double tmp, uint64_t sbits, uint64_t ki) {
+  if ((ki & 0x80000000ull) == 0) {  // k > 0: the exponent of scale may have overflowed
+    const double scale = as_f64(sbits - (1009ull << 52));
+    return fma_(scale, tmp, scale) * 0x1p1009;
+  }
+  const double scale = as_f64(sbits + (1022ull << 52));  // k < 0: subnormal range
+  const double st = tmp * scale;
+  double y = scale + st;
+  if (y < 1.0) {  // round y before scaling it into the subnormal range
+    const double hi = y + 1.0;
+    double lo = (scale - y) + st;
+    const double one_minus_hi = 1.0 - hi;
+    y = (((one_minus_hi + y) + lo) + hi) - 1.0;
+    if (y == 0.0) return 0.0;
+  }
+  return y * 0x1p-1022;
+}
+
+GRT_GLIBC_FN double exp_(double x) {
+  uint32_t abstop = (uint32_t)(as_u64(x) >> 52) & 0x7ffu;
+  if (abstop - 0x3c9u > 0x3eu) {        // |x| < 2^-54 or |x| >= 512 (or inf / nan)
+    if ((int32_t)(abstop - 0x3c9u) < 0) return 1.0 + x;  // tiny |x|
+    if (abstop > 0x408u) {              // |x| >= 1024
+      if (as_u64(x) == 0xfff0000000000000ull) return 0.0;
+      if (abstop == 0x7ffu) return 1.0 + x;  // inf / nan
+      return (as_u64(x) >> 63) ? 0.0 : __builtin_inf();  // __math_uflow / __math_oflow
+    }
+    abstop = 0;                         // 512 <= |x| < 1024: specialcase below
+  }
+  const double kd = fma_(x, EXP_INVLN2N, EXP_SHIFT);
+  const uint64_t ki = as_u64(kd);
+  const double kn = kd - EXP_SHIFT;
+  double r = fma_(kn, EXP_NEGLN2HIN, x);
+  r = fma_(kn, EXP_NEGLN2LON, r);
+  const uint32_t idx = (uint32_t)(ki & 127u) * 2u;
+  const uint64_t top = ki << 45;
+  const double tail = as_f64(GRT_EXPTAB(idx));
+  const uint64_t sbits = GRT_EXPTAB(idx + 1) + top;
+  const double p23 = fma_(r, EXP_C3, EXP_C2);
+  const double tr = r + tail;
+  const double r2 = r * r;
+  const double p45 = fma_(r, EXP_C5, EXP_C4);
+  const double tmp = fma_(r2 * r2, p45, fma_(p23, r2, tr));
+  if (abstop == 0) return exp_special(tmp, sbits, ki);
+  const double scale = as_f64(sbits);
+  return fma_(scale, tmp, scale);
+}
 
 // ---------------------------------------------------------------- sin / cos ----
 // glibc 2.35 __sin_fma / __cos_fma (sysdeps/ieee754/dbl-64/s_sin.c, the IBM accurate

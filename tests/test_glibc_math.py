@@ -67,3 +67,21 @@ def test_device_sin_cos_sincos_are_bit_identical_to_glibc(trig_checkers, mode):
         n, fast, bad = map(int, out.strip().splitlines()[-1].split())
         assert bad == 0, (exe.name, out)
         assert fast == n, (exe.name, TRIG_MODES[mode], fast, n)
+
+
+EXP_MODES = {0: "vertical falloff -(h/thickness)^2", 1: "boundary falloff -1/max(d^2, 1e-4)",
+             2: "attenuation over 60 decades", 3: "subnormal results and the overflow edge", 4: "random bit patterns"}
+
+
+@pytest.fixture(scope="module")
+def exp_checker(tmp_path_factory):
+    return _build(tmp_path_factory, "glibc_exp_check", ("-fno-builtin-exp",))
+
+
+@pytest.mark.parametrize("mode", sorted(EXP_MODES))
+def test_device_exp_is_bit_identical_to_glibc(exp_checker, mode):
+    """exp_ == glibc exp (__exp_fma) on every input, including the special cases (the
+    VolumetricDisc raymarch's falloffs and attenuations, volumetric_disc.rs:97-138, :242-272)."""
+    out = subprocess.run([str(exp_checker), str(mode), "400000"], check=True, capture_output=True, text=True).stdout
+    n, _, bad = map(int, out.strip().splitlines()[-1].split())
+    assert bad == 0, (EXP_MODES[mode], out)
