@@ -12,14 +12,14 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("GRT_LIB", str(PKG_DIR / "lib" / "libgrt.so")))
 
-GRT_ABI_VERSION = 1
+GRT_ABI_VERSION = 2
 GRT_MAX_OBJECTS = 8
 GRT_MAX_HITS = 16
 
 # enums (grt_api.h)
 GEOM_EUCLIDEAN, GEOM_SCHWARZSCHILD, GEOM_KERR, GEOM_KERR_BL, GEOM_EUCLIDEAN_SPHERICAL = 0, 1, 2, 3, 4
 TEX_BITMAP, TEX_CHECKER, TEX_BLACKBODY = 0, 1, 2
-OBJ_SPHERE, OBJ_DISC = 0, 1
+OBJ_SPHERE, OBJ_DISC, OBJ_VOLUMETRIC_DISC = 0, 1, 2
 TEMP_CONSTANT, TEMP_KERR_LUT = 0, 1
 CLASS_ESCAPED, CLASS_CAPTURED, CLASS_HIT = 0, 1, 2
 STATUS_OK, ERR_MAX_STEPS, ERR_NO_CIRCULAR_ORBIT, ERR_BELOW_RISCO, ERR_NON_FINITE_RADIUS = 0, 1, 2, 3, 4
@@ -44,6 +44,11 @@ class ObjectDesc(C.Structure):
         ("temperature", _d), ("inner_radius", _d), ("outer_radius", _d),
         ("temp_constant", _d), ("r_isco", _d), ("lut_r", _pd), ("lut_t", _pd),
         ("lut_n", C.c_uint32), ("_pad2", C.c_uint32), ("texture", TextureDesc),
+        # VolumetricDisc (volumetric_disc.rs:21-95)
+        ("axis", _d * 3), ("thickness", _d), ("march_step_size", _d), ("density_multiplier", _d),
+        ("brightness_reference_temperature", _d), ("absorption", _d), ("scattering", _d),
+        ("noise_scale", _d * 3), ("noise_offset", _d), ("march_max_steps", C.c_uint64),
+        ("num_octaves", C.c_uint32), ("perlin_seed", C.c_uint32),
     ]
 
 
@@ -88,7 +93,8 @@ class AdaptiveConfig(C.Structure):
 class Stats(C.Structure):
     _fields_ = [
         ("accepted_steps", C.c_uint64), ("attempts", C.c_uint64), ("rays", C.c_uint64),
-        ("hit_overflows", C.c_uint64), ("kernel_ms", _d),
+        ("hit_overflows", C.c_uint64), ("kernel_ms", _d), ("march_jobs", C.c_uint64),
+        ("march_samples", C.c_uint64),
     ]
 
 
@@ -153,6 +159,8 @@ def lib() -> C.CDLL:
         "grt_blackbody_lut": (C.c_int, [u32, _pd, _pd]),
         "grt_blackbody_xyz": (None, [_d, _d, _pd]),
         "grt_srgb_to_xyza": (None, [C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8, _pd]),
+        "grt_perlin_permutation": (None, [u32, C.POINTER(C.c_uint8)]),
+        "grt_volumetric_frame": (None, [_pd, _pd, _pd, _pd]),
         "grt_xyz_to_srgb8": (C.c_int, [_pd, C.c_size_t, i32, _d, C.POINTER(C.c_uint8)]),
         "grt_linear_max": (None, [_pd, C.c_size_t, _d, _pd]),
         "grt_xyz_to_srgb": (None, [_pd, _d, C.POINTER(C.c_uint8)]),
@@ -202,7 +210,7 @@ EXPORTED_SYMBOLS = [
     "grt_host_scene_load", "grt_host_geometry_load", "grt_host_scene_desc", "grt_host_scene_adaptive", "grt_host_scene_destroy",
     "grt_camera_build", "grt_stationary_velocity", "grt_zamo_velocity", "grt_cartesian_to_spherical",
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
-    "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_xyz_to_srgb8", "grt_xyz_to_srgb", "grt_blackbody_spectrum", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
+    "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_perlin_permutation", "grt_volumetric_frame", "grt_xyz_to_srgb8", "grt_xyz_to_srgb", "grt_blackbody_spectrum", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
     "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config", "grt_set_schedule",
     "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",

@@ -8,6 +8,7 @@
 // The result is an owned grt_host_scene whose descriptor the device API consumes.
 #include <cerrno>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -51,6 +52,15 @@ bool num(const TomlTable& t, const std::string& k, double* out, std::string& err
     return false;
   }
   *out = v->number();
+  return true;
+}
+bool uint_field(const TomlTable& t, const std::string& k, uint64_t* out, std::string& err) {  // serde usize / u32
+  const TomlValue* v = get(t, k);
+  if (!v || v->kind != TomlValue::Int || v->i < 0) {
+    err = "missing or non-integer field `" + k + "`";
+    return false;
+  }
+  *out = (uint64_t)v->i;
   return true;
 }
 bool triple(const TomlTable& t, const std::string& k, double out[3], std::string& err) {
@@ -373,12 +383,52 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
       if (!num(*ob, "radius", &o.radius, err) || !triple(*ob, "position", o.center, err) ||
           !num(*ob, "temperature", &o.temperature, err))
         return fail("Sphere: " + err);
-    } else if (oname == "Disc") {
-      o.kind = GRT_OBJ_DISC;
+    } else if (oname == "Disc" || oname == "VolumetricDisc") {
+      const bool vol = oname == "VolumetricDisc";
+      o.kind = vol ? GRT_OBJ_VOLUMETRIC_DISC : GRT_OBJ_DISC;
       double temperature;
       if (!num(*ob, "inner_radius", &o.inner_radius, err) || !num(*ob, "outer_radius", &o.outer_radius, err) ||
           !num(*ob, "temperature", &temperature, err))
-        return fail("Disc: " + err);
+        return fail(oname + ": " + err);
+      if (vol) {  // configuration.rs:200-217, validated as cli/shared.rs:238-284
+        uint64_t octaves, msteps, seed = 1;
+        if (!uint_field(*ob, "num_octaves", &octaves, err) || !uint_field(*ob, "max_steps", &msteps, err) ||
+            !num(*ob, "step_size", &o.march_step_size, err) || !num(*ob, "thickness", &o.thickness, err) ||
+            !num(*ob, "density_multiplier", &o.density_multiplier, err) ||
+            !num(*ob, "brightness_reference_temperature", &o.brightness_reference_temperature, err) ||
+            !num(*ob, "absorption", &o.absorption, err) || !num(*ob, "scattering", &o.scattering, err) ||
+            !triple(*ob, "noise_scale", o.noise_scale, err) || !num(*ob, "noise_offset", &o.noise_offset, err))
+          return fail("VolumetricDisc: " + err);
+        if (get(*ob, "perlin_seed") && (!uint_field(*ob, "perlin_seed", &seed, err) || seed > 0xffffffffull))
+          return fail("VolumetricDisc: field `perlin_seed` must be a u32");
+        o.axis[0] = 0.0;
+        o.axis[1] = 0.0;
+        o.axis[2] = 1.0;
+        if (get(*ob, "axis") && !triple(*ob, "axis", o.axis, err)) return fail("VolumetricDisc: " + err);
+        o.num_octaves = (uint32_t)(octaves > 0xffffffffull ? 0xffffffffull : octaves);
+        o.march_max_steps = msteps;
+        o.perlin_seed = (uint32_t)seed;
+        char buf[256];
+        auto bad = [&](const char* what, double v) {
+          snprintf(buf, sizeof buf, "Invalid configuration: VolumetricDisc requires %s (got %s=%g).", what,
+                   what, v);
+          return fail(buf);
+        };
+        if (o.outer_radius <= o.inner_radius) {
+          snprintf(buf, sizeof buf,
+                   "Invalid configuration: VolumetricDisc requires outer_radius > inner_radius (got "
+                   "outer_radius=%g, inner_radius=%g).",
+                   o.outer_radius, o.inner_radius);
+          return fail(buf);
+        }
+        if (o.thickness <= 0.0) return bad("thickness > 0", o.thickness);
+        if (msteps == 0) return fail("Invalid configuration: VolumetricDisc requires max_steps > 0 (got max_steps=0).");
+        if (o.march_step_size <= 0.0) return bad("step_size > 0", o.march_step_size);
+        if (o.brightness_reference_temperature <= 0.0)
+          return bad("brightness_reference_temperature > 0", o.brightness_reference_temperature);
+        if (o.absorption < 0.0) return bad("absorption >= 0", o.absorption);
+        if (o.scattering < 0.0) return bad("scattering >= 0", o.scattering);
+      }
       // geometry.get_temperature_computer (euclidean.rs:219-226, schwarzschild.rs:267-279,
       // kerr.rs:498-510, kerr_bl.rs:412-424)
       if (d.geometry == GRT_GEOM_EUCLIDEAN || d.geometry == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
@@ -391,13 +441,11 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
         double spin = d.geometry == GRT_GEOM_SCHWARZSCHILD ? 0.0 : d.a;
         if (grt_kerr_temperature_lut(temperature, o.outer_radius, spin, d.radius, 1000, hs->lut_r[k].data(),
                                      hs->lut_t[k].data(), &o.r_isco))
-          return fail("Disc temperature LUT: DenominatorCloseToZero / NoCircularOrbitPossible");
+          return fail(oname + " temperature LUT: DenominatorCloseToZero / NoCircularOrbitPossible");
         o.lut_r = hs->lut_r[k].data();
         o.lut_t = hs->lut_t[k].data();
         o.lut_n = 1000;
       }
-    } else if (oname == "VolumetricDisc") {
-      return fail("VolumetricDisc is out of scope for this build (SURVEY.md section 2)");
     } else {
       return fail("unknown object `" + oname + "`");
     }

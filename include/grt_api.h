@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GRT_ABI_VERSION 1
+#define GRT_ABI_VERSION 2
 
 /* ---- enums (values are part of the ABI) -------------------------------------- */
 
@@ -53,10 +53,12 @@ enum grt_texture_kind {
   GRT_TEX_BLACKBODY = 2 /* texture.rs:104-210 BlackBodyMapper (LUT over log10 T) */
 };
 
-/* configuration.rs:188-219 ObjectsConfig (VolumetricDisc is out of scope). */
+/* configuration.rs:188-219 ObjectsConfig. */
 enum grt_object_kind {
-  GRT_OBJ_SPHERE = 0, /* scene_objects/sphere.rs */
-  GRT_OBJ_DISC = 1    /* scene_objects/disc.rs   */
+  GRT_OBJ_SPHERE = 0,          /* scene_objects/sphere.rs                           */
+  GRT_OBJ_DISC = 1,            /* scene_objects/disc.rs                             */
+  GRT_OBJ_VOLUMETRIC_DISC = 2  /* scene_objects/volumetric_disc.rs (Perlin fBm gas,
+                                  constant-step raymarch per intersection)          */
 };
 
 /* rendering/temperature.rs: ConstantTemperatureComputer / KerrTemperatureComputer. */
@@ -127,6 +129,23 @@ typedef struct grt_object_desc {
   uint32_t lut_n;
   uint32_t _pad2;
   grt_texture_desc texture;
+  /* GRT_OBJ_VOLUMETRIC_DISC (volumetric_disc.rs:21-95, configuration.rs:200-217).
+   * inner/outer radius, the temperature model and the texture are the Disc fields
+   * above (cli/shared.rs:219-307 builds it like a Disc).  The axis is the configured
+   * one, (0,0,1) when absent; grt_scene_create normalises it and derives e1, e2
+   * exactly as VolumetricDisc::new (:61-73) and the Perlin permutation table from
+   * perlin_seed (noise 0.9.0 PermutationTable::new, see grt_perlin_permutation). */
+  double axis[3];
+  double thickness;                        /* Gaussian sigma; capture slab 3x this  */
+  double march_step_size;                  /* raymarch step (config step_size)      */
+  double density_multiplier;
+  double brightness_reference_temperature;
+  double absorption, scattering;           /* sigma_a, sigma_s                      */
+  double noise_scale[3];
+  double noise_offset;
+  uint64_t march_max_steps;                /* raymarch samples per intersection     */
+  uint32_t num_octaves;
+  uint32_t perlin_seed;                    /* config perlin_seed, default 1         */
 } grt_object_desc;
 
 /* The camera after Camera::new (camera.rs:151-196): position and velocity in the
@@ -250,6 +269,15 @@ int grt_blackbody_lut(uint32_t n, double* log_t, double* xyz);
 void grt_blackbody_xyz(double temperature, double redshift, double out_xyz[3]);
 /* srgb_to_xyz (color.rs:310-332), alpha := a/255 (CIETristimulus::from_color). */
 void grt_srgb_to_xyza(uint8_t r, uint8_t g, uint8_t b, uint8_t a, double out[4]);
+/* Perlin::new(seed) of the `noise` crate 0.9.0 (volumetric_disc.rs:83), restated from
+ * its published source (the crate is not vendored): PermutationTable::new seeds
+ * rand_xorshift 0.3's XorShiftRng with the words [1, seed, seed, seed] and shuffles
+ * 0..=255 with rand 0.8's SliceRandom::shuffle (Fisher-Yates, gen_range by widening
+ * multiply + rejection).  out[i] = values[i]. */
+void grt_perlin_permutation(uint32_t seed, uint8_t out[256]);
+/* VolumetricDisc::new's frame (volumetric_disc.rs:61-73): the normalised axis
+ * ((0,0,1) when |axis|^2 <= f64::EPSILON) and the in-plane unit vectors e1, e2. */
+void grt_volumetric_frame(const double axis_in[3], double axis[3], double e1[3], double e2[3]);
 /* xyz_to_srgb (color.rs:225-241): one XYZ colour -> sRGB8, linear * exposure, no
  * tone mapping (the `blackbody` subcommand, cli/blackbody.rs:7-25). */
 void grt_xyz_to_srgb(const double xyz[3], double exposure, uint8_t rgb_out[3]);
@@ -278,6 +306,10 @@ typedef struct grt_stats {
   uint64_t rays;
   uint64_t hit_overflows;
   double kernel_ms;        /* hipEvent time of the integration kernel(s)               */
+  /* VolumetricDisc raymarches (volumetric_disc.rs:199-328): one per window-nearest
+   * volumetric intersection whose colour reaches the composite, and their samples. */
+  uint64_t march_jobs;
+  uint64_t march_samples;
 } grt_stats;
 
 /* Optional per-sample sub-pixel offsets (get_ray_for_offset, camera.rs:247-254):

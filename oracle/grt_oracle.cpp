@@ -10,6 +10,8 @@
 //   * Scene::color_of_ray, get_uv_coordinates   src/rendering/scene.rs:114-231
 //   * Objects::intersects, step_at_intersection src/scene_objects/objects.rs:27-120
 //   * Disc / Sphere intersections + emitters    src/scene_objects/{disc,sphere}.rs
+//   * VolumetricDisc (capture cylinder, Perlin fBm density, constant-step raymarch)
+//                                               src/scene_objects/volumetric_disc.rs
 //   * Schwarzschild / Kerr / KerrBL / Euclidean / EuclideanSpherical
 //                                               src/geometry/*.rs (RHS, metrics, stops)
 //   * redshift, textures, temperature lookup    src/rendering/{redshift,texture,temperature}.rs
@@ -870,7 +872,7 @@ static int should_stop(const Geometry& g, const IntegrationConfig& cfg, const do
 }
 
 struct Counters {
-  uint64_t accepted = 0, attempts = 0;
+  uint64_t accepted = 0, attempts = 0, march_samples = 0;
 };
 
 // integrator.rs:78-174.  Returns the stop reason in *stop.
@@ -1109,6 +1111,373 @@ static bool sphere_intersects(const grt_object_desc& o, const Point& ys, const P
   return false;
 }
 
+// ------------------------------------------------------------ volumetric disc ----
+// scene_objects/volumetric_disc.rs.  Its noise is Perlin of the `noise` crate 0.9.0
+// (Cargo.lock; with rand 0.8.7 and rand_xorshift 0.3.0), which is NOT vendored under
+// /root/reference: perlin_3d, PermutationTable and the RNG below restate the crates'
+// published algorithms, so the noise values are "parity unpinned" (no reference test
+// fixes them; the volumetric_disc.rs tests pin the rest, tests/test_oracle_kats.py).
+namespace noise09 {
+struct XorShift {  // rand_xorshift 0.3.0 XorShiftRng::next_u32
+  uint32_t x, y, z, w;
+  uint32_t next_u32() {
+    uint32_t t = x ^ (x << 11);
+    x = y;
+    y = z;
+    z = w;
+    w = w ^ (w >> 19) ^ (t ^ (t >> 8));
+    return w;
+  }
+};
+// rand 0.8 Rng::gen_range(0..n) for u32 = UniformInt::sample_single_inclusive(0, n - 1)
+static uint32_t gen_range(XorShift& rng, uint32_t n) {
+  uint32_t range = n;
+  uint32_t zone = (range << __builtin_clz(range)) - 1u;  // `(range << lz).wrapping_sub(1)`
+  while (true) {
+    uint64_t m = (uint64_t)rng.next_u32() * (uint64_t)range;  // wmul
+    if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+  }
+}
+// permutationtable.rs PermutationTable::new(seed) + Distribution<PermutationTable>
+static void permutation_table(uint32_t seed, uint8_t* values) {
+  uint8_t real[16] = {0};
+  real[0] = 1;
+  for (int i = 1; i < 4; ++i) {
+    real[i * 4] = (uint8_t)seed;
+    real[i * 4 + 1] = (uint8_t)(seed >> 8);
+    real[i * 4 + 2] = (uint8_t)(seed >> 16);
+    real[i * 4 + 3] = (uint8_t)(seed >> 24);
+  }
+  uint32_t w[4];
+  for (int i = 0; i < 4; ++i)  // XorShiftRng::from_seed: little-endian words
+    w[i] = (uint32_t)real[4 * i] | (uint32_t)real[4 * i + 1] << 8 | (uint32_t)real[4 * i + 2] << 16 |
+           (uint32_t)real[4 * i + 3] << 24;
+  XorShift rng{w[0], w[1], w[2], w[3]};
+  for (int i = 0; i < 256; ++i) values[i] = (uint8_t)i;
+  for (int i = 255; i >= 1; --i) {  // SliceRandom::shuffle
+    uint32_t j = gen_range(rng, (uint32_t)i + 1);
+    std::swap(values[i], values[j]);
+  }
+}
+// NoiseHasher for PermutationTable: fold (a & 0xff) with values[a] ^ b, then values[.]
+static inline size_t hash3(const uint8_t* P, int64_t x, int64_t y, int64_t z) {
+  size_t i = (size_t)(x & 0xff);
+  i = (size_t)P[i] ^ (size_t)(y & 0xff);
+  i = (size_t)P[i] ^ (size_t)(z & 0xff);
+  return P[i];
+}
+static inline double gradient_dot_v(size_t perm, double x, double y, double z) {  // core/perlin.rs
+  switch (perm & 15) {
+    case 0: return x + y;
+    case 1: return -x + y;
+    case 2: return x - y;
+    case 3: return -x - y;
+    case 4: return x + z;
+    case 5: return -x + z;
+    case 6: return x - z;
+    case 7: return -x - z;
+    case 8: return y + z;
+    case 9: return -y + z;
+    case 10: return y - z;
+    case 11: return -y - z;
+    case 12: return x + y;
+    case 13: return -x + y;
+    case 14: return -y + z;
+    default: return -y - z;
+  }
+}
+static inline double s_curve5(double x) { return x * x * x * (x * (x * 6.0 - 15.0) + 10.0); }
+// core/perlin.rs perlin_3d (Perlin::get)
+static double perlin_3d(const uint8_t* P, double px, double py, double pz) {
+  const double SCALE_FACTOR = 1.1547005383792515;
+  double fx = std::floor(px), fy = std::floor(py), fz = std::floor(pz);
+  int64_t cx = (int64_t)fx, cy = (int64_t)fy, cz = (int64_t)fz;
+  double dx = px - fx, dy = py - fy, dz = pz - fz;
+  auto g = [&](int ox, int oy, int oz) {
+    return gradient_dot_v(hash3(P, cx + ox, cy + oy, cz + oz), dx - (double)ox, dy - (double)oy, dz - (double)oz);
+  };
+  double g000 = g(0, 0, 0), g100 = g(1, 0, 0), g010 = g(0, 1, 0), g110 = g(1, 1, 0);
+  double g001 = g(0, 0, 1), g101 = g(1, 0, 1), g011 = g(0, 1, 1), g111 = g(1, 1, 1);
+  double a = s_curve5(dx), b = s_curve5(dy), c = s_curve5(dz);
+  double k0 = g000;
+  double k1 = g100 - g000;
+  double k2 = g010 - g000;
+  double k3 = g001 - g000;
+  double k4 = g000 + g110 - g100 - g010;
+  double k5 = g000 + g101 - g100 - g001;
+  double k6 = g000 + g011 - g010 - g001;
+  double k7 = g100 + g010 + g001 + g111 - g000 - g110 - g101 - g011;
+  double result = k0 + k1 * a + k2 * b + k3 * c + k4 * a * b + k5 * a * c + k6 * b * c + k7 * a * b * c;
+  return rust_clamp(result * SCALE_FACTOR, -1.0, 1.0);
+}
+}  // namespace noise09
+
+static inline Vec3 cross3(const Vec3& a, const Vec3& b) {  // nalgebra Vector3::cross
+  return Vec3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+static inline Vec3 normalize3(const Vec3& v) {  // nalgebra normalize = v / |v|
+  double n = norm3(v);
+  return Vec3{v.x / n, v.y / n, v.z / n};
+}
+static inline double rust_max(double a, double b) { return std::fmax(a, b); }  // f64::max
+
+enum CylKind { NoIntersection, Parallel, OneIntersection, TwoIntersections };
+struct Cyl {
+  CylKind k;
+  double t1, t2;
+};
+
+struct VDisc {  // volumetric_disc.rs:21-95
+  const grt_object_desc* o = nullptr;
+  Vec3 axis, e1, e2;
+  uint8_t perm[256];
+  double g_fbm;  // (-h).exp2() with h = 0.5 (fbm's only call, :130)
+  void init(const grt_object_desc* od) {
+    o = od;
+    Vec3 ax{od->axis[0], od->axis[1], od->axis[2]};
+    axis = dot3(ax, ax) <= 2.220446049250313e-16 ? Vec3{0.0, 0.0, 1.0} : normalize3(ax);
+    Vec3 seed = std::fabs(axis.x) > 0.9 ? Vec3{0.0, 1.0, 0.0} : Vec3{1.0, 0.0, 0.0};
+    e1 = normalize3(cross3(seed, axis));
+    e2 = normalize3(cross3(axis, e1));
+    noise09::permutation_table(od->perlin_seed, perm);
+    g_fbm = std::exp2(-0.5);
+  }
+  double noise(double x, double y, double z) const { return noise09::perlin_3d(perm, x, y, z); }
+  double fbm(const Vec3& x) const {  // :330-342
+    double frequency = 4.0, amplitude = 1.0, t = 0.0;
+    for (uint32_t i = 0; i < o->num_octaves; ++i) {
+      t += amplitude * noise(x.x * frequency, x.y * frequency, x.z * frequency);
+      frequency *= 2.0;
+      amplitude *= g_fbm;
+    }
+    return t;
+  }
+  double compute_density(const Vec3& p) const {  // :97-138
+    double h = std::fabs(dot3(p, axis));
+    double r = norm3(cross3(p, axis));
+    double rin = o->inner_radius, rout = o->outer_radius;
+    if (r <= rin || r >= rout) return 0.0;
+    double q = h / o->thickness;
+    double vertical_falloff = std::exp(-(q * q));
+    if (vertical_falloff < 0.001) return 0.0;
+    double radial_base = std::pow(rin / r, 1.5);
+    double boundary_falloff = 1.0;
+    double d1 = rout - r, d2 = r - rin;
+    boundary_falloff *= std::exp(-1.0 / rust_max(d1 * d1, 0.0001));
+    boundary_falloff *= std::exp(-1.0 / rust_max(d2 * d2, 0.0001));
+    double x_local = dot3(p, e1);
+    double y_local = dot3(p, e2);
+    double phi = std::atan2(y_local, x_local);
+    double sp, cp;
+    g_sincos(phi, &sp, &cp);  // phi.cos() and phi.sin() in one block: one sincos
+    double noise_phi_x = cp * o->noise_scale[1];
+    double noise_phi_y = sp * o->noise_scale[1];
+    double n = fbm(Vec3{r * o->noise_scale[0], noise_phi_x, noise_phi_y});
+    n += noise(r * 0.5, h * o->noise_scale[2], cp) * 0.5;
+    double n2 = rust_max(n + o->noise_offset, 0.0) * o->density_multiplier;
+    return n2 * radial_base * vertical_falloff * boundary_falloff;
+  }
+  void get_uv(const Vec3& p, double* u, double* v) const {  // :140-152
+    double x = dot3(p, e1), y = dot3(p, e2);
+    double rr = std::sqrt(x * x + y * y);
+    double phi = std::atan2(y, x);
+    double r = (rr - o->inner_radius) / (o->outer_radius - o->inner_radius);
+    double sp, cp;
+    g_sincos(phi, &sp, &cp);
+    *u = 0.5 + 0.5 * r * cp;
+    *v = 0.5 + 0.5 * r * sp;
+  }
+  Cyl clipped_cylinder(const Vec3& from, const Vec3& to, double radius, double half_height) const {  // :348-405
+    Vec3 sv{to.x - from.x, to.y - from.y, to.z - from.z};
+    double len = norm3(sv);
+    if (len < 1e-12) return Cyl{NoIntersection, 0, 0};
+    Vec3 d{sv.x / len, sv.y / len, sv.z / len};
+    Vec3 v = cross3(from, axis);
+    Vec3 w = cross3(d, axis);
+    double a = dot3(w, w);
+    double b = 2.0 * dot3(v, w);
+    double c = dot3(v, v) - radius * radius;
+    if (a < 1e-10) {
+      if (dot3(v, v) > radius * radius) return Cyl{NoIntersection, 0, 0};
+      return Cyl{Parallel, 0, 0};
+    }
+    double disc = b * b - 4.0 * a * c;
+    if (disc < 0.0) return Cyl{NoIntersection, 0, 0};
+    double sq = std::sqrt(disc);
+    double dists[2] = {(-b - sq) / (2.0 * a), (-b + sq) / (2.0 * a)};
+    double hits[2];
+    int nh = 0;
+    for (double dist : dists) {
+      double t = dist / len;
+      if (0.0 <= t && t <= 1.0) {
+        Vec3 p{from.x + t * sv.x, from.y + t * sv.y, from.z + t * sv.z};
+        if (std::fabs(dot3(p, axis)) <= half_height) hits[nh++] = t;
+      }
+    }
+    if (nh == 0) return Cyl{NoIntersection, 0, 0};
+    if (nh == 1) return Cyl{OneIntersection, hits[0], 0};
+    return Cyl{TwoIntersections, std::fmin(hits[0], hits[1]), std::fmax(hits[0], hits[1])};
+  }
+  bool cap(const Vec3& from, const Vec3& to, double radius, double pos, double* t_out) const {  // :407-440
+    Vec3 sv{to.x - from.x, to.y - from.y, to.z - from.z};
+    double len = norm3(sv);
+    if (len < 1e-12) return false;
+    Vec3 n{sv.x / len, sv.y / len, sv.z / len};
+    double denom = dot3(n, axis);
+    if (std::fabs(denom) < 1e-10) return false;
+    double t = (pos - dot3(from, axis)) / dot3(sv, axis);
+    if (!(0.0 <= t && t <= 1.0)) return false;
+    Vec3 p{from.x + t * sv.x, from.y + t * sv.y, from.z + t * sv.z};
+    Vec3 c = cross3(p, axis);
+    if (dot3(c, c) > radius * radius) return false;
+    *t_out = t;
+    return true;
+  }
+  Cyl cylinder(const Vec3& from, const Vec3& to) const {  // intersects_cylinder :442-494
+    double rin = o->inner_radius, rout = o->outer_radius;
+    std::vector<double> hits;
+    Vec3 dir{to.x - from.x, to.y - from.y, to.z - from.z};
+    double capture_height = o->thickness * 3.0;
+    for (double radius : {rout, rin}) {
+      Cyl c = clipped_cylinder(from, to, radius, capture_height);
+      if (c.k == OneIntersection) hits.push_back(c.t1);
+      else if (c.k == TwoIntersections) { hits.push_back(c.t1); hits.push_back(c.t2); }
+    }
+    for (double pos : {capture_height, -capture_height}) {
+      double t;
+      if (cap(from, to, rout, pos, &t)) {
+        Vec3 p{from.x + t * dir.x, from.y + t * dir.y, from.z + t * dir.z};
+        Vec3 c = cross3(p, axis);
+        if (dot3(c, c) >= rin * rin) hits.push_back(t);
+      }
+    }
+    auto total_key = [](double x) {  // f64::total_cmp order
+      uint64_t u;
+      std::memcpy(&u, &x, 8);
+      return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+    };
+    std::stable_sort(hits.begin(), hits.end(), [&](double a, double b) { return total_key(a) < total_key(b); });
+    if (hits.empty()) return Cyl{NoIntersection, 0, 0};
+    if (hits.size() == 1) return Cyl{OneIntersection, hits[0], 0};
+    return Cyl{TwoIntersections, hits[0], hits[1]};
+  }
+  // Hittable::intersects (:506-578): first capture-boundary crossing with t > 1e-9
+  bool intersects(const Vec3& s, const Vec3& e, double* t_out, Vec3* point, Vec3* direction) const {
+    Vec3 dir{e.x - s.x, e.y - s.y, e.z - s.z};
+    Cyl c = cylinder(s, e);
+    double t;
+    const double MIN_T = 1e-9;
+    if (c.k == NoIntersection || c.k == Parallel) return false;
+    if (c.k == OneIntersection) {
+      if (!(c.t1 > MIN_T)) return false;
+      t = c.t1;
+    } else {
+      if (c.t1 > MIN_T) t = c.t1;
+      else if (c.t2 > MIN_T) t = c.t2;
+      else return false;
+    }
+    if (!(0.0 <= t && t <= 1.0)) return false;  // error! + None
+    *t_out = t;
+    *point = Vec3{s.x + t * dir.x, s.y + t * dir.y, s.z + t * dir.z};
+    *direction = dir;
+    return true;
+  }
+  bool precompute_exit_distance(const Vec3& ro, const Vec3& rd, double* out) const {  // :172-196
+    double max_distance = o->march_step_size * (double)o->march_max_steps;
+    Vec3 to{ro.x + rd.x * max_distance, ro.y + rd.y * max_distance, ro.z + rd.z * max_distance};
+    Cyl c = cylinder(ro, to);
+    const double MIN_T = 1e-9;
+    if (c.k == OneIntersection) {
+      if (c.t1 > MIN_T) { *out = c.t1 * max_distance; return true; }
+      return false;
+    }
+    if (c.k == TwoIntersections) {
+      if (c.t1 > MIN_T) { *out = c.t1 * max_distance; return true; }
+      if (c.t2 > MIN_T) { *out = c.t2 * max_distance; return true; }
+    }
+    return false;
+  }
+  bool does_exit(const Vec3& p, const Vec3& rd, double t) const {  // :154-170
+    Vec3 to{p.x + rd.x * t, p.y + rd.y * t, p.z + rd.z * t};
+    double ti;
+    Vec3 ip, dir;
+    if (!intersects(p, to, &ti, &ip, &dir)) return false;
+    return ti > 1e-9;
+  }
+};
+
+struct FrequencyData {  // redshift.rs RayFrequencyData
+  double observer_energy, p_t, p_phi;
+};
+
+// Geometry::circular_orbit_killing_coefficients of a Cartesian point (euclidean.rs:207-217,
+// euclidean_spherical.rs:191-201, schwarzschild.rs:260-265, kerr.rs:487-496, kerr_bl.rs:398-410)
+static Err killing_at(const Geometry& g, int32_t geometry, const Point& cart, Killing* k) {
+  if (geometry == GRT_GEOM_EUCLIDEAN || geometry == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
+    k->u_t = 1.0;
+    k->u_phi = 0.0;
+    return OK;
+  }
+  double spin = geometry == GRT_GEOM_SCHWARZSCHILD ? 0.0 : g.a;
+  return killing_coefficients(g.radius, spin, g.radial_coordinate(cart), k);
+}
+
+// raymarch_constant_step_internal (:209-328).  Returns the error that the reference's
+// `?` would propagate (color_at_uv then substitutes (0,0,0,0), :596-600).
+static Err vdisc_raymarch(const VDisc& V, const TextureMap& tex, const Geometry& g, int32_t geometry,
+                          const Vec3& ro, const Vec3& rd, const FrequencyData& f, bool use_cached_exit,
+                          XYZA* out, uint64_t* samples) {
+  const grt_object_desc& o = *V.o;
+  double sigma_a = o.absorption, sigma_s = o.scattering;
+  XYZA acc{0.0, 0.0, 0.0, 0.0};
+  double transparency = 1.0, alpha_weighted_sum = 0.0, alpha_weight_total = 0.0;
+  double d_s = o.march_step_size, d_o = 0.0;
+  double exit_distance = 0.0;
+  bool cached = use_cached_exit && V.precompute_exit_distance(ro, rd, &exit_distance);
+  for (uint64_t i = 0; i < o.march_max_steps; ++i) {
+    Vec3 p{ro.x + rd.x * d_o, ro.y + rd.y * d_o, ro.z + rd.z * d_o};
+    d_o += d_s;
+    if (samples) ++*samples;
+    double density = V.compute_density(p);
+    if (density > 0.0) {
+      double sample_attenuation = std::exp(-d_s * density * (sigma_a + sigma_s));
+      transparency *= sample_attenuation;
+      Killing k;
+      if (killing_at(g, geometry, Point{CS::Cartesian, 0.0, {0.0, p.x, p.y, p.z}}, &k) == OK) {
+        double emitter_energy = k.u_t * f.p_t + k.u_phi * f.p_phi;
+        double redshift = f.observer_energy / emitter_energy;
+        double r_dist = norm3(cross3(p, V.axis));
+        double temperature;
+        Err e = compute_temperature(o, r_dist, &temperature);
+        if (e != OK) return e;
+        double u, v;
+        V.get_uv(p, &u, &v);
+        XYZA light = tex.color_at_uv(u, v, redshift, temperature);
+        double travel_density = d_s;
+        double light_attenuation = std::exp(-density * travel_density * (sigma_a + sigma_s));
+        double ratio = temperature / o.brightness_reference_temperature;
+        double r2 = ratio * ratio;
+        double intensity_factor = r2 * r2;  // powi(4)
+        double emission_weight = transparency * light_attenuation * sigma_s * density * d_s;
+        double wgt = emission_weight * intensity_factor;
+        double alpha_sample_weight = density * d_s;
+        alpha_weighted_sum += rust_clamp(light.alpha, 0.0, 1.0) * alpha_sample_weight;
+        alpha_weight_total += alpha_sample_weight;
+        acc.x += light.x * wgt;
+        acc.y += light.y * wgt;
+        acc.z += light.z * wgt;
+      }
+    }
+    bool exited = cached ? d_o >= exit_distance : V.does_exit(p, rd, d_s);
+    if (exited) break;
+  }
+  double physical_opacity = 1.0 - transparency;
+  double texture_alpha = alpha_weight_total > 0.0 ? alpha_weighted_sum / alpha_weight_total : 1.0;
+  acc.alpha = physical_opacity * texture_alpha;
+  *out = acc;
+  return OK;
+}
+
 struct SceneCtx {
   const grt_scene_desc* d;
   std::unique_ptr<Geometry> g;
@@ -1117,6 +1486,7 @@ struct SceneCtx {
   Point cam_position;
   TextureMap celestial;
   TextureMap obj_tex[GRT_MAX_OBJECTS];
+  VDisc vd[GRT_MAX_OBJECTS];  // VolumetricDisc frames + permutation tables
 };
 
 // objects.rs:27-44
@@ -1132,8 +1502,9 @@ static Step step_at_intersection(const Geometry& g, const Step& a, const Step& b
 }
 
 // objects.rs:65-120
-static Err objects_intersects(const SceneCtx& S, const Step& ys, const Step& ye, double observer_energy,
-                              bool* has, XYZA* color) {
+static Err objects_intersects(const SceneCtx& S, const Step& ys, const Step& ye, const FrequencyData& freq,
+                              bool* has, XYZA* color, uint64_t* march_samples) {
+  const double observer_energy = freq.observer_energy;
   const Geometry& g = *S.g;
   *has = false;
   double shortest = std::numeric_limits<double>::max();
@@ -1141,7 +1512,15 @@ static Err objects_intersects(const SceneCtx& S, const Step& ys, const Step& ye,
   for (uint32_t k = 0; k < S.d->n_objects; ++k) {
     const grt_object_desc& o = S.d->objects[k];
     Intersection in;
-    bool hit = o.kind == GRT_OBJ_DISC ? disc_intersects(o, ys.x, ye.x, &in) : sphere_intersects(o, ys.x, ye.x, &in);
+    Vec3 vdir{0.0, 0.0, 0.0};
+    bool hit;
+    if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {  // volumetric_disc.rs:506-578
+      Vec3 vp{0.0, 0.0, 0.0};
+      hit = S.vd[k].intersects(spatial_cartesian(ys.x), spatial_cartesian(ye.x), &in.t, &vp, &vdir);
+      in.point = Point{CS::Cartesian, 0.0, {0.0, vp.x, vp.y, vp.z}};
+    } else {
+      hit = o.kind == GRT_OBJ_DISC ? disc_intersects(o, ys.x, ye.x, &in) : sphere_intersects(o, ys.x, ye.x, &in);
+    }
     if (!hit) continue;
     Vec3 ip = spatial_cartesian(in.point);
     Vec3 dv{ip.x - ysc.x, ip.y - ysc.y, ip.z - ysc.z};
@@ -1150,7 +1529,7 @@ static Err objects_intersects(const SceneCtx& S, const Step& ys, const Step& ye,
       shortest = distance;
       Step st = step_at_intersection(g, ys, ye, in.point, in.t);
       FourVector vel;
-      if (o.kind == GRT_OBJ_DISC) {  // disc.rs:101-110
+      if (o.kind != GRT_OBJ_SPHERE) {  // disc.rs:101-110, volumetric_disc.rs:603-612
         Err e = g.circular_orbit_velocity(st.x, &vel);
         if (e != OK) return e;
       } else {  // sphere.rs:141-150
@@ -1160,17 +1539,42 @@ static Err objects_intersects(const SceneCtx& S, const Step& ys, const Step& ye,
       double sig0 = g.signature0();
       double redshift = (sig0 * observer_energy) / (sig0 * emitter_energy);  // redshift.rs:36-38
       double temperature;
-      if (o.kind == GRT_OBJ_DISC) {
+      if (o.kind != GRT_OBJ_SPHERE) {  // disc.rs:112-120, volumetric_disc.rs:614-622
         Err e = compute_temperature(o, g.radial_coordinate(in.point), &temperature);
         if (e != OK) return e;
       } else {
         temperature = o.temperature;
       }
-      *color = S.obj_tex[k].color_at_uv(in.u, in.v, redshift, temperature);
+      if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {  // color_at_uv (:580-601): raymarch from the hit
+        Vec3 rd = normalize3(vdir);
+        XYZA c;
+        if (vdisc_raymarch(S.vd[k], S.obj_tex[k], g, S.d->geometry, ip, rd, freq, true, &c, march_samples) != OK)
+          c = XYZA{0.0, 0.0, 0.0, 0.0};  // unwrap_or_else
+        *color = c;
+      } else {
+        *color = S.obj_tex[k].color_at_uv(in.u, in.v, redshift, temperature);
+      }
       *has = true;
     }
   }
   return OK;
+}
+
+// RedshiftComputer::get_ray_frequency_data (redshift.rs:45-60) with the geometries'
+// axial_killing_vector (euclidean.rs:203-205, kerr.rs:482-485: (0, -y, x, 0);
+// schwarzschild.rs:256-258, euclidean_spherical.rs:187-189, kerr_bl.rs:394-396: d_phi)
+static FrequencyData ray_frequency_data(const SceneCtx& S, const Ray& ray, double observer_energy) {
+  const Geometry& g = *S.g;
+  FrequencyData f;
+  f.observer_energy = observer_energy;
+  FourVector e_t{ray.momentum.cs, {1.0, 0.0, 0.0, 0.0}};
+  f.p_t = g.inner_product(ray.position, e_t, ray.momentum);
+  int32_t geo = S.d->geometry;
+  FourVector ax = (geo == GRT_GEOM_EUCLIDEAN || geo == GRT_GEOM_KERR)
+                      ? FourVector{CS::Cartesian, {0.0, -ray.position[2], ray.position[1], 0.0}}
+                      : FourVector{g.cs(), {0.0, 0.0, 0.0, 1.0}};
+  f.p_phi = g.inner_product(ray.position, ax, ray.momentum);
+  return f;
 }
 
 // camera.rs:214-232
@@ -1223,12 +1627,13 @@ static Err color_of_ray(const SceneCtx& S, const Ray& ray, Sample* out, Counters
   out->stop = stop;
   if (e != OK) return e;
   double observer_energy = g.inner_product(ray.position, S.cam_velocity, ray.momentum);  // redshift.rs:40-43
+  FrequencyData freq = ray_frequency_data(S, ray, observer_energy);
   double object_opacity = 0.0;
   std::vector<XYZA> intersections;
   for (size_t w = 0; w + 1 < steps.size(); ++w) {
     bool has;
     XYZA c;
-    Err ie = objects_intersects(S, steps[w], steps[w + 1], observer_energy, &has, &c);
+    Err ie = objects_intersects(S, steps[w], steps[w + 1], freq, &has, &c, &cnt->march_samples);
     if (ie != OK) return ie;
     if (has) {
       intersections.push_back(c);
@@ -1278,7 +1683,10 @@ static void init_ctx(SceneCtx& S, const grt_scene_desc* d) {
   S.cam_position = Point{S.g->cs(), d->a, {d->camera.position[0], d->camera.position[1], d->camera.position[2], d->camera.position[3]}};
   S.cam_velocity = FourVector{S.g->cs(), {d->camera.velocity[0], d->camera.velocity[1], d->camera.velocity[2], d->camera.velocity[3]}};
   S.celestial = TextureMap{&d->celestial, d};
-  for (uint32_t k = 0; k < d->n_objects && k < GRT_MAX_OBJECTS; ++k) S.obj_tex[k] = TextureMap{&d->objects[k].texture, d};
+  for (uint32_t k = 0; k < d->n_objects && k < GRT_MAX_OBJECTS; ++k) {
+    S.obj_tex[k] = TextureMap{&d->objects[k].texture, d};
+    if (d->objects[k].kind == GRT_OBJ_VOLUMETRIC_DISC) S.vd[k].init(&d->objects[k]);
+  }
 }
 
 static void default_sample(Sample* s) {
@@ -1590,12 +1998,52 @@ int oracle_object_intersects(const grt_scene_desc* d, int object, const double* 
   const grt_object_desc& o = d->objects[object];
   Point pa{CS::Cartesian, 0.0, {a[0], a[1], a[2], a[3]}}, pb{CS::Cartesian, 0.0, {b[0], b[1], b[2], b[3]}};
   Intersection in;
-  bool hit = o.kind == GRT_OBJ_DISC ? disc_intersects(o, pa, pb, &in) : sphere_intersects(o, pa, pb, &in);
+  bool hit;
+  if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
+    VDisc V;
+    V.init(&o);
+    Vec3 vp{0.0, 0.0, 0.0}, dir;
+    hit = V.intersects(spatial_cartesian(pa), spatial_cartesian(pb), &in.t, &vp, &dir);
+    in.point = Point{CS::Cartesian, 0.0, {0.0, vp.x, vp.y, vp.z}};
+  } else {
+    hit = o.kind == GRT_OBJ_DISC ? disc_intersects(o, pa, pb, &in) : sphere_intersects(o, pa, pb, &in);
+  }
   if (hit) {
     for (int k = 0; k < 4; ++k) point_out[k] = in.point.v[k];
     *t_out = in.t;
   }
   return hit ? 1 : 0;
+}
+
+// ---- VolumetricDisc pieces (volumetric_disc.rs tests, :693-786) ----
+void oracle_perlin_table(uint32_t seed, uint8_t* out) { noise09::permutation_table(seed, out); }
+double oracle_perlin(uint32_t seed, double x, double y, double z) {
+  uint8_t P[256];
+  noise09::permutation_table(seed, P);
+  return noise09::perlin_3d(P, x, y, z);
+}
+double oracle_vdisc_density(const grt_scene_desc* d, int object, const double* p) {
+  VDisc V;
+  V.init(&d->objects[object]);
+  return V.compute_density(Vec3{p[0], p[1], p[2]});
+}
+// raymarch_constant_step_internal with frequency (observer_energy, p_t, p_phi); returns
+// the propagated error (0 = Ok) and the colour in out4.
+int oracle_vdisc_raymarch(const grt_scene_desc* d, int object, const double* ro, const double* rd,
+                          const double* freq3, int use_cached_exit, double* out4, uint64_t* samples) {
+  SceneCtx S;
+  init_ctx(S, d);
+  FrequencyData f{freq3[0], freq3[1], freq3[2]};
+  XYZA c{0.0, 0.0, 0.0, 0.0};
+  uint64_t n = 0;
+  Err e = vdisc_raymarch(S.vd[object], S.obj_tex[object], *S.g, d->geometry, Vec3{ro[0], ro[1], ro[2]},
+                         Vec3{rd[0], rd[1], rd[2]}, f, use_cached_exit != 0, &c, &n);
+  out4[0] = c.x;
+  out4[1] = c.y;
+  out4[2] = c.z;
+  out4[3] = c.alpha;
+  if (samples) *samples = n;
+  return e;
 }
 
 // ---- output stage (color.rs:193-298), as Raytracer::render_section calls it for

@@ -53,6 +53,12 @@ def lib():
         L.oracle_killing_coefficients.argtypes = [_d, _d, _d, _pd, _pd]
         L.oracle_object_intersects.argtypes = [vp, C.c_int, _pd, _pd, _pd, _pd]
         L.oracle_xyz_to_srgb8.argtypes = [_pd, C.c_uint64, C.c_int, _d, _u8p]
+        L.oracle_perlin_table.argtypes = [C.c_uint32, _u8p]
+        L.oracle_perlin.restype = _d
+        L.oracle_perlin.argtypes = [C.c_uint32, _d, _d, _d]
+        L.oracle_vdisc_density.restype = _d
+        L.oracle_vdisc_density.argtypes = [vp, C.c_int, _pd]
+        L.oracle_vdisc_raymarch.argtypes = [vp, C.c_int, _pd, _pd, _pd, C.c_int, _pd, _u64p]
         _lib = L
     return _lib
 
@@ -181,3 +187,27 @@ def xyz_to_srgb8(xyza, tone: int, exposure: float = 1.0):
     out = np.zeros((x.shape[0], 3), np.uint8)
     lib().oracle_xyz_to_srgb8(_dp(x), x.shape[0], tone, exposure, out.ctypes.data_as(_u8p))
     return out
+
+
+# ---- VolumetricDisc pieces (volumetric_disc.rs) ----
+def perlin_table(seed: int) -> np.ndarray:
+    out = np.zeros(256, np.uint8)
+    lib().oracle_perlin_table(seed, out.ctypes.data_as(_u8p))
+    return out
+
+
+def perlin(seed: int, x: float, y: float, z: float) -> float:
+    return lib().oracle_perlin(seed, x, y, z)
+
+
+def vdisc_density(desc, obj: int, p) -> float:
+    return lib().oracle_vdisc_density(_addr(desc), obj, _dp(np.asarray(p, np.float64)))
+
+
+def vdisc_raymarch(desc, obj: int, ro, rd, freq=(1.0, 1.0, 0.0), cached=True):
+    out = np.zeros(4)
+    n = C.c_uint64()
+    err = lib().oracle_vdisc_raymarch(_addr(desc), obj, _dp(np.asarray(ro, np.float64)),
+                                      _dp(np.asarray(rd, np.float64)), _dp(np.asarray(freq, np.float64)),
+                                      1 if cached else 0, _dp(out), C.byref(n))
+    return err, out, n.value

@@ -71,7 +71,7 @@ BASE = (SCENES / "schwarzschild.toml").read_text()
     (lambda s: s + "\n[adaptive_sampling]\nluminance_contrast_threshold = 1.5\n", "luminance_contrast_threshold"),
     (lambda s: s.replace('path = "resources/disk.png"', 'path = "resources/missing.png"'), "missing.png"),
     (lambda s: s.replace("inner_radius = 3.0", "inner_radius = 3.0 3.0"), "TOML"),
-    (lambda s: s.replace("objects.Sphere", "objects.VolumetricDisc"), "out of scope"),
+    (lambda s: s.replace("objects.Sphere", "objects.VolumetricDisc"), "inner_radius"),
 ])
 def test_invalid_scenes_are_rejected(grt, tmp_path, mutation, needle):
     p = _write_scene(tmp_path, mutation(BASE))
