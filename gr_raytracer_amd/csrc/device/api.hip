@@ -49,12 +49,15 @@ struct DeviceCopy {
   std::vector<void*> allocations;
   unsigned long long* d_counter = nullptr;  // [0] work counter
   unsigned long long* d_stats = nullptr;    // [0..3] accepted, attempts, rays, overflows
+  unsigned long long* d_march = nullptr;    // [0] jobs, [1] job cursor, [2] samples, [3] jobs (cumulative)
+  bool vol = false;                         // the scene has VolumetricDiscs
   int cus = 0;
   int blocks = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // calls on one device are serialised
   // integrate -> shade hand-off buffers, grown on demand (bytes per ray: ~1.1 KB)
   uint64_t ws_cap = 0;
+  bool ws_vol = false;  // the arena holds the volumetric arrays
   void* ws_mem = nullptr;
   // tile-order scratch (probe counts, keys, indices, order, radix-sort temp), grow-only
   uint64_t sched_tiles = 0;
@@ -64,19 +67,23 @@ struct DeviceCopy {
 // Carve a Workspace for n rays out of the device's grow-only arena.
 int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   const uint64_t M = GRT_MAX_HITS;
-  const uint64_t per_ray = 8 * 8 + 4 * 8 + 1 + 1 + 1 + 4 + M * (4 + 1 + 4 * 8 + 3 * 8);
-  if (n > dc.ws_cap) {
+  const bool vol = dc.vol;
+  // volumetric scenes: rc grows to 6 doubles; chord directions, raymarched colours, jobs
+  const uint64_t per_ray = 8 * 8 + (vol ? 6 : 4) * 8 + 1 + 1 + 1 + 4 + M * (4 + 1 + 4 * 8 + 3 * 8) +
+                           (vol ? M * (3 * 8 + 4 * 8 + 8) : 0);
+  if (n > dc.ws_cap || (vol && !dc.ws_vol)) {
     if (dc.ws_mem) {
       (void)hipDeviceSynchronize();  // earlier async launches may still use the old arena
       (void)hipFree(dc.ws_mem);
     }
     dc.ws_mem = nullptr;
     uint64_t cap = std::max<uint64_t>(n, 1 << 16);
-    if (hipMalloc(&dc.ws_mem, cap * per_ray + 1024) != hipSuccess) {
+    if (hipMalloc(&dc.ws_mem, cap * per_ray + 32 * 256) != hipSuccess) {  // + per-array alignment
       dc.ws_cap = 0;
       return fail(-ENOMEM, "cannot allocate the integrate/shade workspace");
     }
     dc.ws_cap = cap;
+    dc.ws_vol = vol;
   }
   uint64_t cap = dc.ws_cap;
   char* p = (char*)dc.ws_mem;
@@ -87,7 +94,7 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   };
   ws->n = n;
   ws->y = (double*)take(8 * 8 * cap);
-  ws->rc = (double*)take(4 * 8 * cap);
+  ws->rc = (double*)take((vol ? 6 : 4) * 8 * cap);
   ws->rec_p = (double*)take(4 * M * 8 * cap);
   ws->rec_pt = (double*)take(3 * M * 8 * cap);
   ws->steps = (uint32_t*)take(4 * cap);
@@ -96,6 +103,14 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   ws->status = (uint8_t*)take(cap);
   ws->nrec = (uint8_t*)take(cap);
   ws->rec_obj = (uint8_t*)take(M * cap);
+  ws->rec_dir = ws->vcol = nullptr;
+  ws->jobs = nullptr;
+  ws->march = dc.d_march;
+  if (vol) {
+    ws->rec_dir = (double*)take(3 * M * 8 * cap);
+    ws->vcol = (double*)take(4 * M * 8 * cap);
+    ws->jobs = (uint64_t*)take(M * 8 * cap);
+  }
   // the kernels index with the launch's n, which must not exceed the carved capacity
   if (n > cap) return fail(-ENOMEM, "workspace too small");
   return 0;
@@ -259,6 +274,37 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     if ((rc = upload(dc, s->lut_t[k].data(), s->lut_t[k].size(), &lt))) return rc;
     q.lut_r = lr;
     q.lut_t = lt;
+    if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {  // VolumetricDisc::new (volumetric_disc.rs:43-95)
+      dc.vol = true;
+      ds.has_vol = 1;
+      grt_volumetric_frame(o.axis, q.ax, q.e1, q.e2);
+      grt_perlin_permutation(o.perlin_seed, ds.perm[k]);
+      q.perm_slot = k;
+      q.thickness = o.thickness;
+      q.cap_h = o.thickness * 3.0;
+      q.m_step = o.march_step_size;
+      q.m_max = o.march_max_steps;
+      q.m_maxdist = o.march_step_size * (double)o.march_max_steps;
+      q.dens_mult = o.density_multiplier;
+      q.bref = o.brightness_reference_temperature;
+      q.sig_a = o.absorption;
+      q.sig_s = o.scattering;
+      q.noff = o.noise_offset;
+      q.g_fbm = std::exp2(-0.5);
+      for (int i = 0; i < 3; ++i) q.ns[i] = o.noise_scale[i];
+      q.octaves = o.num_octaves;
+      // far-field filter bounds (geodesic.hip vol_far)
+      const double corner = std::sqrt(o.outer_radius * o.outer_radius + q.cap_h * q.cap_h);
+      q.vol_far_r = 2.0 * corner * (1.0 + 1e-6);
+      q.vol_rmax = 1e6 * q.cap_h;
+      q.vol_slab_h = q.cap_h * (1.0 + 1e-6) + 1e-12;
+      q.vol_slab_ok = (q.ax[0] == 0.0 && q.ax[1] == 0.0 && q.ax[2] == 1.0) ? 1 : 0;
+      if (!std::isfinite(q.vol_far_r) || !std::isfinite(q.vol_rmax) || !(q.cap_h > 0.0)) {
+        q.vol_far_r = HUGE_VAL;
+        q.vol_rmax = 0.0;
+        q.vol_slab_ok = 0;
+      }
+    }
     fill_dev_texture(o.texture, q.tex);
     uint32_t* ot = nullptr;
     if ((rc = upload(dc, s->obj_tex[k].rgba.data(), s->obj_tex[k].rgba.size(), &ot))) return rc;
@@ -276,10 +322,12 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   if ((rc = upload(dc, &ds, 1, &dsp))) return rc;
   dc.d_scene = dsp;
   void* p = nullptr;
-  HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&p, 16 * sizeof(unsigned long long)));
   dc.allocations.push_back(p);
+  HIP_TRY(hipMemset(p, 0, 16 * sizeof(unsigned long long)));
   dc.d_counter = (unsigned long long*)p;
   dc.d_stats = dc.d_counter + 1;
+  dc.d_march = dc.d_counter + 8;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   dc.cus = prop.multiProcessorCount;
@@ -369,6 +417,7 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
     if (rc0) return rc0;
   }
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
+  if (dc.vol) HIP_TRY(hipMemsetAsync(dc.d_march, 0, 2 * sizeof(unsigned long long), stream));  // jobs, cursor
   int threads = g_threads;
   int blocks = g_blocks_per_cu > 0 ? dc.cus * g_blocks_per_cu : dc.blocks;
   // never launch more lanes than there is work for
@@ -379,7 +428,7 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   int rc = ensure_workspace(dc, n_out, &ws);
   if (rc) return rc;
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
-                            stream));
+                            dc.vol, stream));
   return 0;
 }
 
@@ -412,10 +461,16 @@ int validate_desc(const grt_scene_desc* d) {
   if ((rc = check_tex(d->celestial))) return rc;
   for (uint32_t k = 0; k < d->n_objects; ++k) {
     const grt_object_desc& o = d->objects[k];
-    if (o.kind != GRT_OBJ_SPHERE && o.kind != GRT_OBJ_DISC) return fail(-EINVAL, "unknown object kind");
+    if (o.kind != GRT_OBJ_SPHERE && o.kind != GRT_OBJ_DISC && o.kind != GRT_OBJ_VOLUMETRIC_DISC)
+      return fail(-EINVAL, "unknown object kind");
     if ((rc = check_tex(o.texture))) return rc;
-    if (o.kind == GRT_OBJ_DISC && o.temp_kind == GRT_TEMP_KERR_LUT && (o.lut_n < 2 || !o.lut_r || !o.lut_t))
+    if (o.kind != GRT_OBJ_SPHERE && o.temp_kind == GRT_TEMP_KERR_LUT && (o.lut_n < 2 || !o.lut_r || !o.lut_t))
       return fail(-EINVAL, "disc temperature LUT missing");
+    if (o.kind == GRT_OBJ_VOLUMETRIC_DISC &&
+        (!(o.outer_radius > o.inner_radius) || !(o.thickness > 0.0) || o.march_max_steps == 0 ||
+         !(o.march_step_size > 0.0) || !(o.brightness_reference_temperature > 0.0) || !(o.absorption >= 0.0) ||
+         !(o.scattering >= 0.0)))
+      return fail(-EINVAL, "invalid VolumetricDisc parameters (cli/shared.rs:238-284)");
   }
   if (d->camera.rows <= 0 || d->camera.cols <= 0) return fail(-EINVAL, "camera has no pixels");
   return 0;
@@ -515,6 +570,7 @@ static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, u
                  (uint32_t*)b_steps.p, (uint8_t*)b_stop.p};
   hipStream_t st = nullptr;
   HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 4 * sizeof(unsigned long long), st));
   HIP_TRY(hipEventRecord(dc->ev0, st));
   if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
   HIP_TRY(hipEventRecord(dc->ev1, st));
@@ -535,6 +591,10 @@ static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, u
     stats->rays = h[2];
     stats->hit_overflows = h[3];
     stats->kernel_ms = ms;
+    unsigned long long m[4];
+    HIP_TRY(hipMemcpy(m, dc->d_march, sizeof(m), hipMemcpyDeviceToHost));
+    stats->march_jobs = m[3];
+    stats->march_samples = m[2];
   }
   return 0;
 }
@@ -677,6 +737,7 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
   if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n)) || (rc = b_x64.alloc(n * 32)))
     return rc;
   HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 4 * sizeof(unsigned long long), st));
   HIP_TRY(hipEventRecord(dc->ev0, st));
   grt::WorkList wl = rect_worklist(from_row, from_col, h, w);
   grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p, nullptr, nullptr};
@@ -769,6 +830,10 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
     stats->rays = hs[2];
     stats->hit_overflows = hs[3];
     stats->kernel_ms = ms;
+    unsigned long long m[4];
+    HIP_TRY(hipMemcpy(m, dc->d_march, sizeof(m), hipMemcpyDeviceToHost));
+    stats->march_jobs = m[3];
+    stats->march_samples = m[2];
   }
   return 0;
 }

@@ -34,6 +34,19 @@ struct DevObject {
   uint32_t lut_n;
   uint32_t _pad;
   DevTexture tex;
+  // VolumetricDisc (volumetric_disc.rs:21-95), derived on the host (api.hip)
+  double ax[3], e1[3], e2[3];  // normalised axis and in-plane frame (:61-73)
+  double thickness, cap_h;     // Gaussian sigma; capture half-height thickness * 3.0 (:454)
+  double m_step, m_maxdist;    // raymarch step; step_size * max_steps as f64 (:173)
+  uint64_t m_max;              // raymarch samples per intersection
+  double dens_mult, bref, sig_a, sig_s, noff, g_fbm;  // g_fbm = (-0.5).exp2() (:331), host libm
+  double ns[3];                // noise_scale
+  uint32_t octaves, perm_slot; // fBm octaves; index of this object's table in DevScene::perm
+  // exact far-field window filter for the capture region (geodesic.hip window_far):
+  // vol_far_r = 2 * |capture corner| * (1 + 1e-6); vol_rmax bounds the radii it is
+  // used at; vol_slab_h = cap_h * (1 + 1e-6) + 1e-12 (axis == z only, vol_slab_ok)
+  double vol_far_r, vol_rmax, vol_slab_h;
+  int32_t vol_slab_ok, _pad2;
 };
 
 struct DevCamera {
@@ -76,7 +89,10 @@ struct DevScene {
   uint32_t bb_n;
   uint32_t _pad1;
   const double* srgb_lin;  // 256 entries
+  int32_t has_vol;         // any GRT_OBJ_VOLUMETRIC_DISC: integrate records chord directions and
+  int32_t _pad2;           // the frequency data (p_t, p_phi), the shade pass raymarches
   DevObject obj[8];
+  uint8_t perm[8][256];    // Perlin permutation tables (noise 0.9.0 PermutationTable), per object
 };
 
 // Work description for one launch.
@@ -99,7 +115,7 @@ struct WorkList {
 struct Workspace {
   uint64_t n;
   double* y;          // [8][n]
-  double* rc;         // [4][n]
+  double* rc;         // [4][n], [6][n] with volumetric objects (+ p_t, p_phi)
   uint8_t* stop;      // [n]
   uint8_t* status;    // [n]
   uint8_t* nrec;      // [n] candidates recorded (saturating at 255)
@@ -108,6 +124,11 @@ struct Workspace {
   uint8_t* rec_obj;   // [MAX][n] object index
   double* rec_p;      // [4][MAX][n] momentum lerped to the hit (objects.rs:27-44)
   double* rec_pt;     // [3][MAX][n] hit point (sphere-local for spheres)
+  // volumetric scenes only (NULL otherwise)
+  double* rec_dir;    // [3][MAX][n] chord direction y_end - y_start (volumetric candidates)
+  double* vcol;       // [4][MAX][n] raymarched colour of volumetric candidate slots
+  uint64_t* jobs;     // [MAX * n] raymarch jobs: (ray << 8) | candidate slot
+  unsigned long long* march;  // [0] job count, [1] job cursor, [2] samples, [3] jobs done
 };
 
 // Local row -> frame row under cyclic row-band sharding: band k of shard s is frame

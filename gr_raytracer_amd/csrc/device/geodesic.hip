@@ -151,6 +151,7 @@ GDEV XYZA blend(const XYZA& self, const XYZA& other) {
 struct RayConst {
   double obs;
   double e, lz, q;
+  double pt, pphi;  // RayFrequencyData p_t, p_phi (redshift.rs:45-60), volumetric scenes only
 };
 
 // =========================================================== geometry kernels ======
@@ -708,6 +709,8 @@ GDEV int compute_temperature(const DevObject& o, double radius, double* out) {
   return GRT_OK;
 }
 
+#include "volumetric.h"
+
 
 // ====================================================== window (chord) tests ======
 // Geometry only: the integrate kernel decides hit / no hit, the chord parameter t and
@@ -847,6 +850,19 @@ GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayCons
   camera_momentum(cam, row, col, p);
   init_state<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, p, y, rc);
   rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
+  rc.pt = 0.0;
+  rc.pphi = 0.0;
+  if (S.has_vol) {  // get_ray_frequency_data: <e_t, p> and <axial Killing vector, p>
+    const double et[4] = {1.0, 0.0, 0.0, 0.0};
+    double ax[4] = {0.0, 0.0, 0.0, 1.0};  // d_phi (schwarzschild.rs:256, kerr_bl.rs:394, ...)
+    if constexpr (G == GRT_GEOM_EUCLIDEAN || G == GRT_GEOM_KERR) {  // (0, -y, x, 0), kerr.rs:482-485
+      ax[1] = -cam.pos[2];
+      ax[2] = cam.pos[1];
+      ax[3] = 0.0;
+    }
+    rc.pt = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, et, p);
+    rc.pphi = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, ax, p);
+  }
 }
 
 // integrator.rs:203-268
@@ -897,6 +913,42 @@ GDEV int should_stop(const DevScene& S, const double* y, double* c, bool& c_vali
 //  * Sphere (sphere.rs:37-128): a hit needs |x - c|^2 - R^2 to change sign over the
 //    window; |x| in [r, r + far_a] outside the host's shell [shell_lo, shell_hi]
 //    (1e-9 margins) keeps both ends strictly outside.
+//  * VolumetricDisc (volumetric_disc.rs:442-494): every hit lies in the capture region
+//    |x.axis| <= cap_h, |x x axis| <= rout.  Skipped when (1) the chord stays farther than
+//    vol_far_r = 2 |capture corner| (1 + 1e-6) from the origin: |x| >= r at both ends and
+//    the chord is no longer than the chart path, |dr| + (r_max + far_a)(|dtheta| + |dphi|)
+//    (the map's partial derivatives are bounded by 1, r + |a|, r + |a|); or (2) for the z
+//    axis, both ends in one hemisphere with |z| = r |cos theta| >= r (2/pi) x (Jordan's
+//    inequality, x = distance of theta to the equator) beyond cap_h (1 + 1e-6): z is
+//    linear along the chord, so it never enters the slab.  Only for radii below
+//    vol_rmax = 1e6 cap_h, where the chord arithmetic's rounding is far below the margins.
+GDEV bool vol_far(const DevScene& S, const DevObject& o, const double* ya, const double* yb) {
+  const double ra = ya[1], rb = yb[1];
+  if (!(ra > 0.0 && rb > 0.0)) return false;
+  const double rmax = fmax(ra, rb);
+  if (!(rmax < o.vol_rmax)) return false;
+  const double L = fabs(rb - ra) + (rmax + S.far_a) * (fabs(yb[2] - ya[2]) + fabs(yb[3] - ya[3]));
+  if (fmin(ra, rb) > o.vol_far_r + L * (1.0 + 1e-9)) return true;
+  if (!o.vol_slab_ok) return false;
+  constexpr double N_LO = -1.5707963257948966, N_HI = 1.5707963257948966;  // (-pi/2, pi/2) -/+ 1e-9
+  constexpr double S_LO = 1.5707963277948966, S_HI = 4.7123889793846899;   // (pi/2, 3pi/2) +/- 1e-9
+  constexpr double HALF_PI = 1.5707963267948966, TWO_OVER_PI = 0.63661977236758134;
+  const double ta = ya[2], tb = yb[2];
+  double xa, xb;
+  if (ta > N_LO && ta < N_HI && tb > N_LO && tb < N_HI) {
+    xa = HALF_PI - fabs(ta);
+    xb = HALF_PI - fabs(tb);
+  } else if (ta > S_LO && ta < S_HI && tb > S_LO && tb < S_HI) {
+    xa = HALF_PI - fabs(ta - PI);
+    xb = HALF_PI - fabs(tb - PI);
+  } else {
+    return false;
+  }
+  const double za = ra * TWO_OVER_PI * (xa - 1e-15) * (1.0 - 1e-9);
+  const double zb = rb * TWO_OVER_PI * (xb - 1e-15) * (1.0 - 1e-9);
+  return za > o.vol_slab_h && zb > o.vol_slab_h;
+}
+
 template <int G>
 GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
   if constexpr (G != GRT_GEOM_SCHWARZSCHILD && G != GRT_GEOM_KERR_BL && G != GRT_GEOM_EUCLIDEAN_SPHERICAL) {
@@ -913,6 +965,8 @@ GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
         bool south = ta > S_LO && ta < S_HI && tb > S_LO && tb < S_HI;
         if (!(north || south)) return false;
         if (!(ra >= 1e-3 * rb && rb >= 1e-3 * ra && ra > 0.0)) return false;
+      } else if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
+        if (!vol_far(S, o, ya, yb)) return false;
       } else {
         bool out_a = ra > o.shell_hi || fabs(ra) + S.far_a < o.shell_lo;
         bool out_b = rb > o.shell_hi || fabs(rb) + S.far_a < o.shell_lo;
@@ -979,7 +1033,7 @@ GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, int stop
 // order (objects.rs:81) and the stop test.  A window hit nearer than the current
 // nearest (objects.rs:86-88) is recorded as a candidate: its object, window index,
 // hit point and the lerped momentum (objects.rs:27-44).
-template <int G>
+template <int G, bool VOL>
 __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     const DevScene* __restrict__ Sp, WorkList wl, Workspace ws, unsigned long long* __restrict__ counter,
     unsigned long long* __restrict__ stats) {
@@ -1047,6 +1101,10 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
             ws.rc[1 * n + idx] = rc.e;
             ws.rc[2 * n + idx] = rc.lz;
             ws.rc[3 * n + idx] = rc.q;
+            if constexpr (VOL) {
+              ws.rc[4 * n + idx] = rc.pt;
+              ws.rc[5 * n + idx] = rc.pphi;
+            }
             c_valid = false;
             h = S.step_size;
             h_cur = rclamp(h, H_MIN, H_MAX);
@@ -1099,10 +1157,12 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
       for (uint32_t k = 0; k < S.n_objects; ++k) {
         const DevObject& o = S.obj[k];
         double t, pt[3];
-        bool hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
+        bool hit;
+        if (VOL && o.kind == GRT_OBJ_VOLUMETRIC_DISC) hit = vdisc_chord(o, c, cn, &t, pt);
+        else hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
         if (!hit) continue;
         double wx = pt[0], wy = pt[1], wz = pt[2];
-        if (o.kind != GRT_OBJ_DISC) {
+        if (o.kind == GRT_OBJ_SPHERE) {
           wx = pt[0] + o.cx;
           wy = pt[1] + o.cy;
           wz = pt[2] + o.cz;
@@ -1123,6 +1183,11 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
           for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
 #pragma unroll
           for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
+          if constexpr (VOL) {  // chord direction for the raymarch (volumetric_disc.rs:576, :589-594)
+            ws.rec_dir[slot] = cn[0] - c[0];
+            ws.rec_dir[(uint64_t)GRT_MAX_HITS * n + slot] = cn[1] - c[1];
+            ws.rec_dir[(uint64_t)2 * GRT_MAX_HITS * n + slot] = cn[2] - c[2];
+          }
         }
         nrec++;
       }
@@ -1321,11 +1386,18 @@ hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& w
 // ============================================================ shade kernel =======
 // Evaluate one recorded candidate: the emitter step at the intersection
 // (objects.rs:27-44 + :95-115), its redshift, temperature and texture colour.
+// A VolumetricDisc candidate gets its energy and temperature (and their errors) here;
+// its colour is the raymarch of march_kernel (volumetric_disc.rs:580-601), so *col is
+// left untouched.  color = false: errors only (the job-gathering pass).
 template <int G>
 GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o, const double* p,
-                      const double* pt, XYZA* col) {
-  double u_tex, v_tex, wx, wy, wz;
-  if (o.kind == GRT_OBJ_DISC) {  // disc.rs:60-76 uv from the in-plane point
+                      const double* pt, XYZA* col, bool color = true) {
+  double u_tex = 0.0, v_tex = 0.0, wx, wy, wz;
+  if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {  // world hit point (its uv is not used for colour)
+    wx = pt[0];
+    wy = pt[1];
+    wz = pt[2];
+  } else if (o.kind == GRT_OBJ_DISC) {  // disc.rs:60-76 uv from the in-plane point
     wx = pt[0];
     wy = pt[1];
     wz = pt[2];
@@ -1361,7 +1433,7 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
     x[3] = wz;
   }
   double u[4];
-  if (o.kind == GRT_OBJ_DISC) {  // disc.rs:101-110: circular-orbit emitter
+  if (o.kind != GRT_OBJ_SPHERE) {  // disc.rs:101-110, volumetric_disc.rs:603-612: circular-orbit emitter
     if constexpr (G == GRT_GEOM_EUCLIDEAN || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // at rest in flat space
       u[0] = 1.0; u[1] = 0.0; u[2] = 0.0; u[3] = 0.0;
     } else {
@@ -1386,7 +1458,7 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
   double sig0 = signature0<G>();
   double redshift = (sig0 * rc.obs) / (sig0 * em);  // redshift.rs:36-38
   double temperature;
-  if (o.kind == GRT_OBJ_DISC) {
+  if (o.kind != GRT_OBJ_SPHERE) {  // disc.rs:112-120, volumetric_disc.rs:614-622
     double rad;  // get_radial_coordinate of the Cartesian intersection point
     if constexpr (G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) {
       rad = sqrt(ks_r_sqr(S.a, wx, wy, wz));
@@ -1398,7 +1470,7 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
   } else {
     temperature = o.temperature;
   }
-  *col = texture_color(S, o.tex, u_tex, v_tex, redshift, temperature);
+  if (color && o.kind != GRT_OBJ_VOLUMETRIC_DISC) *col = texture_color(S, o.tex, u_tex, v_tex, redshift, temperature);
   return GRT_OK;
 }
 
@@ -1418,15 +1490,64 @@ GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, in
   if (out.stop) out.stop[idx] = (uint8_t)stop;
 }
 
+// Volumetric scenes, pass 1: the candidate slots whose raymarched colour the composite
+// needs -- the window-nearest VolumetricDisc hits of a ray whose window pass raises no
+// error (an error aborts the pixel, scene.rs:146, so its marches would be wasted).
+template <int G>
+GDEV uint32_t march_slots(const DevScene& S, const Workspace& ws, uint64_t idx) {
+  const uint64_t n = ws.n;
+  if (ws.status[idx] != GRT_OK) return 0u;
+  RayConst rc{ws.rc[idx], ws.rc[n + idx], ws.rc[2 * n + idx], ws.rc[3 * n + idx]};
+  uint32_t nrec = ws.nrec[idx];
+  uint32_t nr = nrec < GRT_MAX_HITS ? nrec : GRT_MAX_HITS;
+  uint32_t mask = 0u;
+  for (uint32_t j = 0; j < nr; ++j) {
+    const uint64_t slot = (uint64_t)j * n + idx;
+    uint32_t win = ws.rec_win[slot];
+    const DevObject& o = S.obj[ws.rec_obj[slot]];
+    double p[4], pt[3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot];
+    XYZA col;
+    if (shade_record<G>(S, rc, o, p, pt, &col, false) != GRT_OK) return 0u;
+    bool last_in_window = (j + 1 == nr) || (ws.rec_win[slot + n] != win);
+    if (last_in_window && o.kind == GRT_OBJ_VOLUMETRIC_DISC) mask |= 1u << j;
+  }
+  return mask;
+}
+
 // Scene::color_of_ray's window pass, terminal colour and composite (scene.rs:141-219),
 // one lane per ray, over the candidates the integrate kernel recorded.
-template <int G>
+//   MODE 0: scenes without volumetric objects.
+//   MODE 1: volumetric scenes, pass 1 -- append the raymarch jobs (wave-aggregated).
+//   MODE 2: volumetric scenes, pass 3 -- composite with the raymarched colours (ws.vcol).
+template <int G, int MODE>
 __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__ Sp, Workspace ws, Outputs out,
                                                     unsigned long long* __restrict__ stats) {
   const DevScene& S = *Sp;
   glibc::tables_to_lds();  // whole block, before the early return
   const uint64_t n = ws.n;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (MODE == 1) {
+    const uint32_t mask = idx < n ? march_slots<G>(S, ws, idx) : 0u;
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = __popc(mask);
+    uint32_t incl = c;  // inclusive wave prefix sum of the job counts
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && total) base = atomicAdd(ws.march, (unsigned long long)total);
+    base = __shfl(base, 63);
+    uint64_t pos = base + incl - c;
+    for (uint32_t m = mask; m; m &= m - 1u) ws.jobs[pos++] = (idx << 8) | (uint64_t)__ffs(m) - 1u;
+    return;
+  }
   if (idx >= n) return;
   int status = ws.status[idx];
   int stop = ws.stop[idx];
@@ -1451,13 +1572,19 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot];
 #pragma unroll
     for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot];
-    XYZA col;
+    XYZA col{0.0, 0.0, 0.0, 0.0};
     int e = shade_record<G>(S, rc, o, p, pt, &col);
     if (e != GRT_OK) {  // any window error aborts the pixel (scene.rs:146, objects.rs:96-102)
       write_out(out, idx, fail, GRT_CLASS_ESCAPED, e, stop, steps);
       return;
     }
     bool last_in_window = (j + 1 == nr) || (ws.rec_win[slot + n] != win);
+    if constexpr (MODE == 2) {
+      if (last_in_window && o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
+        const uint64_t MN = (uint64_t)GRT_MAX_HITS * n;
+        col = XYZA{ws.vcol[slot], ws.vcol[MN + slot], ws.vcol[2 * MN + slot], ws.vcol[3 * MN + slot]};
+      }
+    }
     if (last_in_window) {  // the window's nearest hit
       hits[nh++] = col;
       double alpha = rclamp(col.a, 0.0, 1.0);
@@ -1505,34 +1632,50 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
 }
 
 // ------------------------------------------------------------------ launch -------
+// Plain scenes: integrate -> shade.  Volumetric scenes: integrate -> gather raymarch
+// jobs -> march (persistent, lane refill) -> composite; ws.march must be zeroed.
 template <int G>
 static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
                            unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
-                           hipStream_t stream) {
-  hipLaunchKernelGGL(integrate_kernel<G>, dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws, d_counter,
-                     d_stats);
+                           bool vol, hipStream_t stream) {
+  const unsigned nb = (unsigned)((ws.n + 255) / 256);
+  if (!vol) {
+    hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
+                       d_counter, d_stats);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((shade_kernel<G, 0>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+    return hipGetLastError();
+  }
+  if (!ws.rec_dir || !ws.vcol || !ws.jobs || !ws.march) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((integrate_kernel<G, true>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
+                     d_counter, d_stats);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  unsigned nb = (unsigned)((ws.n + 255) / 256);
-  hipLaunchKernelGGL(shade_kernel<G>, dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+  hipLaunchKernelGGL((shade_kernel<G, 1>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL((march_kernel<G>), dim3(blocks), dim3(256), 0, stream, d_scene, ws);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL((shade_kernel<G, 2>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
   return hipGetLastError();
 }
 
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
-                        int threads, hipStream_t stream) {
+                        int threads, bool vol, hipStream_t stream) {
   if (ws.n == 0) return hipSuccess;
   switch (geometry) {
     case GRT_GEOM_EUCLIDEAN:
-      return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
+      return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, stream);
     case GRT_GEOM_SCHWARZSCHILD:
-      return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
+      return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
+                                              stream);
     case GRT_GEOM_KERR:
-      return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
+      return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, stream);
     case GRT_GEOM_KERR_BL:
-      return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, stream);
+      return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, stream);
     case GRT_GEOM_EUCLIDEAN_SPHERICAL:
-      return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads,
+      return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
                                                     stream);
     default:
       return hipErrorInvalidValue;

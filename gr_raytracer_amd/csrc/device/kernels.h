@@ -6,10 +6,12 @@
 
 namespace grt {
 
-// integrate_kernel (persistent, lane refill) then shade_kernel, both on `stream`.
+// integrate_kernel (persistent, lane refill) then shade_kernel, all on `stream`.  With
+// `vol` (the scene has VolumetricDiscs): integrate, job gathering, march_kernel and the
+// composite; the workspace then needs its volumetric arrays, ws.march zeroed.
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
-                        int blocks, int threads, hipStream_t stream);
+                        int blocks, int threads, bool vol, hipStream_t stream);
 
 // Work-order probe: steps of one ray per 8x8 tile of `wl` (rectangle mode), capped.
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,

@@ -120,7 +120,8 @@ class RenderResult:
 
 def _stats_dict(st: L.Stats) -> dict:
     return {"accepted_steps": int(st.accepted_steps), "attempts": int(st.attempts), "rays": int(st.rays),
-            "hit_overflows": int(st.hit_overflows), "kernel_ms": float(st.kernel_ms)}
+            "hit_overflows": int(st.hit_overflows), "kernel_ms": float(st.kernel_ms),
+            "march_jobs": int(st.march_jobs), "march_samples": int(st.march_samples)}
 
 
 class Scene:

@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNEL = "grt::integrate_kernel<1>"
+KERNEL = "grt::integrate_kernel<1, false>"
 
 
 def load(pass_dir):

@@ -1,0 +1,48 @@
+"""Time VolumetricDisc frames on the GPU (SURVEY.md 8(f) row 3 measurement).
+
+usage: python tools/vol_time.py [width] [scene ...]
+For each scene: one warm-up and two timed 1-spp frames through grt_render_pixels (host
+outputs), printing accepted RKF45 steps, raymarch jobs / samples and the kernel time
+(HIP events around integrate + job gather + march + composite), as one JSON line each.
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+
+import gr_raytracer_amd as g  # noqa: E402
+from conftest import RESOURCES, SCENES, c2_opts, c3_opts  # noqa: E402
+
+SCENES_DEFAULT = ["schwarzschild-volumetric-stony.toml", "schwarzschild-volumetric-dense.toml",
+                  "kerr-bl-volumetric-stony.toml", "kerr-bl-volumetric-streaky.toml"]
+
+
+def main():
+    width = int(sys.argv[1]) if len(sys.argv) > 1 else 1500
+    names = sys.argv[2:] or SCENES_DEFAULT
+    for name in names:
+        opts = (c3_opts if name.startswith("kerr") else c2_opts)(g, width=width, height=width)
+        hs = g.HostScene(str(SCENES / name), opts, str(RESOURCES))
+        sc = g.Scene(hs.desc_ptr(), keepalive=hs)
+        sc.render_pixels(aux=False)
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            r = sc.render_pixels(aux=False)
+            wall = time.perf_counter() - t0
+            if best is None or r.stats["kernel_ms"] < best[0].stats["kernel_ms"]:
+                best = (r, wall)
+        r, wall = best
+        st = r.stats
+        print(json.dumps({"scene": name, "pixels": width * width, "kernel_ms": st["kernel_ms"], "wall_s": wall,
+                          "accepted_steps": st["accepted_steps"], "march_jobs": st["march_jobs"],
+                          "march_samples": st["march_samples"],
+                          "hit_pixels": int((r.ray_class == 2).sum()),
+                          "march_samples_per_s": st["march_samples"] / (st["kernel_ms"] * 1e-3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
