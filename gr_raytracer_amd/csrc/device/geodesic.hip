@@ -843,7 +843,7 @@ GDEV void init_state(const DevScene& S, const double* pos, double st, double ct,
 
 // Create a camera ray's state (camera.rs:234-254 + init_state); also the observer
 // energy the redshift needs (redshift.rs:40-43).
-template <int G>
+template <int G, bool FREQ = false>
 GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayConst& rc) {
   const DevCamera& cam = S.cam;
   double p[4];
@@ -852,7 +852,7 @@ GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayCons
   rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
   rc.pt = 0.0;
   rc.pphi = 0.0;
-  if (S.has_vol) {  // get_ray_frequency_data: <e_t, p> and <axial Killing vector, p>
+  if constexpr (FREQ) {  // get_ray_frequency_data: <e_t, p> and <axial Killing vector, p>
     const double et[4] = {1.0, 0.0, 0.0, 0.0};
     double ax[4] = {0.0, 0.0, 0.0, 1.0};  // d_phi (schwarzschild.rs:256, kerr_bl.rs:394, ...)
     if constexpr (G == GRT_GEOM_EUCLIDEAN || G == GRT_GEOM_KERR) {  // (0, -y, x, 0), kerr.rs:482-485
@@ -949,7 +949,7 @@ GDEV bool vol_far(const DevScene& S, const DevObject& o, const double* ya, const
   return za > o.vol_slab_h && zb > o.vol_slab_h;
 }
 
-template <int G>
+template <int G, bool VOL>
 GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
   if constexpr (G != GRT_GEOM_SCHWARZSCHILD && G != GRT_GEOM_KERR_BL && G != GRT_GEOM_EUCLIDEAN_SPHERICAL) {
     return false;
@@ -965,7 +965,7 @@ GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
         bool south = ta > S_LO && ta < S_HI && tb > S_LO && tb < S_HI;
         if (!(north || south)) return false;
         if (!(ra >= 1e-3 * rb && rb >= 1e-3 * ra && ra > 0.0)) return false;
-      } else if (o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
+      } else if (VOL && o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
         if (!vol_far(S, o, ya, yb)) return false;
       } else {
         bool out_a = ra > o.shell_hi || fabs(ra) + S.far_a < o.shell_lo;
@@ -1096,7 +1096,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
             idx = (uint64_t)r * wl.cols + cc;
           }
           if (valid) {
-            init_ray<G>(S, row, col, y, rc);
+            init_ray<G, VOL>(S, row, col, y, rc);
             ws.rc[0 * n + idx] = rc.obs;
             ws.rc[1 * n + idx] = rc.e;
             ws.rc[2 * n + idx] = rc.lz;
@@ -1148,7 +1148,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     h = h_next;
     i++;
     n_acc++;
-    if (!window_far<G>(S, y, yn)) {
+    if (!window_far<G, VOL>(S, y, yn)) {
       if (!c_valid) to_cart<G>(S, y, c);
       double cn[3];
       to_cart<G>(S, yn, cn);
