@@ -155,7 +155,7 @@ def main() -> None:
         att_per_launch = attempts / args.steps
         flop_per_launch = f_att * att_per_launch + f_step * acc_per_launch
         achieved_tflops = flop_per_launch / (kernel_ms * 1e-3) / 1e12
-        prof = ROOT / "profiles" / "r01c_pmc.json"  # PMC passes of this kernel, tools/run_pmc.sh
+        prof = ROOT / "profiles" / "r01f_pmc.json"  # PMC passes of this kernel, tools/run_pmc.sh
         traffic = None
         if prof.exists():
             try:
@@ -183,7 +183,7 @@ def main() -> None:
                        "frame_wall_s_per_gpu": elapsed / args.steps},
             "roofline": {"bound": "valu-fp64", "achieved": achieved_tflops, "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": traffic, "kernel": "grt::integrate_kernel<1> (Schwarzschild; events also span shade_kernel<1>, <0.01%)",
+                         "traffic": traffic, "kernel": "grt::integrate_kernel<1, false> (Schwarzschild; events also span shade_kernel<1, 0>, <0.01%)",
                          "kernel_ms": kernel_ms, "flop_per_launch": flop_per_launch,
                          "flop_model": f"{f_att:g}*attempts + {f_step:g}*accepted (SURVEY 8d)",
                          "hbm_algorithmic_GBps": n * BYTES_PER_PIXEL_OUT / (kernel_ms * 1e-3) / 1e9,

@@ -94,7 +94,7 @@ class Stats(C.Structure):
     _fields_ = [
         ("accepted_steps", C.c_uint64), ("attempts", C.c_uint64), ("rays", C.c_uint64),
         ("hit_overflows", C.c_uint64), ("kernel_ms", _d), ("march_jobs", C.c_uint64),
-        ("march_samples", C.c_uint64),
+        ("march_samples", C.c_uint64), ("march_noise_samples", C.c_uint64), ("march_emit_samples", C.c_uint64),
     ]
 
 

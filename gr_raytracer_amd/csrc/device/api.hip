@@ -570,7 +570,7 @@ static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, u
                  (uint32_t*)b_steps.p, (uint8_t*)b_stop.p};
   hipStream_t st = nullptr;
   HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
-  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
   HIP_TRY(hipEventRecord(dc->ev0, st));
   if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
   HIP_TRY(hipEventRecord(dc->ev1, st));
@@ -591,10 +591,12 @@ static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, u
     stats->rays = h[2];
     stats->hit_overflows = h[3];
     stats->kernel_ms = ms;
-    unsigned long long m[4];
+    unsigned long long m[8];
     HIP_TRY(hipMemcpy(m, dc->d_march, sizeof(m), hipMemcpyDeviceToHost));
     stats->march_jobs = m[3];
     stats->march_samples = m[2];
+    stats->march_noise_samples = m[4];
+    stats->march_emit_samples = m[5];
   }
   return 0;
 }
@@ -737,7 +739,7 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
   if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n)) || (rc = b_x64.alloc(n * 32)))
     return rc;
   HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
-  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
   HIP_TRY(hipEventRecord(dc->ev0, st));
   grt::WorkList wl = rect_worklist(from_row, from_col, h, w);
   grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p, nullptr, nullptr};
@@ -830,10 +832,12 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
     stats->rays = hs[2];
     stats->hit_overflows = hs[3];
     stats->kernel_ms = ms;
-    unsigned long long m[4];
+    unsigned long long m[8];
     HIP_TRY(hipMemcpy(m, dc->d_march, sizeof(m), hipMemcpyDeviceToHost));
     stats->march_jobs = m[3];
     stats->march_samples = m[2];
+    stats->march_noise_samples = m[4];
+    stats->march_emit_samples = m[5];
   }
   return 0;
 }

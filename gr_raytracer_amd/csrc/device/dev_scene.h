@@ -128,7 +128,8 @@ struct Workspace {
   double* rec_dir;    // [3][MAX][n] chord direction y_end - y_start (volumetric candidates)
   double* vcol;       // [4][MAX][n] raymarched colour of volumetric candidate slots
   uint64_t* jobs;     // [MAX * n] raymarch jobs: (ray << 8) | candidate slot
-  unsigned long long* march;  // [0] job count, [1] job cursor, [2] samples, [3] jobs done
+  unsigned long long* march;  // [0] job count, [1] job cursor, [2] samples, [3] jobs (cumulative),
+                              // [4] samples that evaluated the noise, [5] samples that emitted
 };
 
 // Local row -> frame row under cyclic row-band sharding: band k of shard s is frame

@@ -630,10 +630,8 @@ GDEV XYZA texel(const DevScene& S, const DevTexture& t, uint32_t x, uint32_t y) 
   return c;
 }
 
-GDEV XYZA sample_blackbody(const DevScene& S, double temperature) {  // texture.rs:149-195
-  uint32_t n = S.bb_n;
-  const double* lt = S.bb_log_t;
-  const double* c = S.bb_xyz;
+// texture.rs:149-195 over a (log10 T, XYZ) table in global memory or LDS
+GDEV XYZA sample_blackbody_lut(const double* lt, const double* c, uint32_t n, double temperature) {
   double log_t = log10(fmax(temperature, 10.0));
   if (!isfinite(log_t) || log_t <= lt[0]) return XYZA{c[0], c[1], c[2], 1.0};
   if (log_t >= lt[n - 1]) return XYZA{c[3 * (n - 1)], c[3 * (n - 1) + 1], c[3 * (n - 1) + 2], 1.0};
@@ -649,10 +647,14 @@ GDEV XYZA sample_blackbody(const DevScene& S, double temperature) {  // texture.
   double t = (log_t - lt0) / (lt1 - lt0);
   return XYZA{c0[0] + t * (c1[0] - c0[0]), c0[1] + t * (c1[1] - c0[1]), c0[2] + t * (c1[2] - c0[2]), 1.0};
 }
+GDEV XYZA sample_blackbody(const DevScene& S, double temperature) {
+  return sample_blackbody_lut(S.bb_log_t, S.bb_xyz, S.bb_n, temperature);
+}
 
-// TextureMap::color_at_uv (texture.rs:93-257)
-GDEV XYZA texture_color(const DevScene& S, const DevTexture& t, double u, double v, double redshift,
-                        double temperature) {
+// TextureMap::color_at_uv (texture.rs:93-257); bb_lt / bb_xyz: the blackbody table
+// (S.bb_log_t / S.bb_xyz, or an LDS copy of it)
+GDEV XYZA texture_color_lut(const DevScene& S, const DevTexture& t, double u, double v, double redshift,
+                            double temperature, const double* bb_lt, const double* bb_xyz) {
   XYZA c;
   if (t.kind == GRT_TEX_BITMAP) {
     uint32_t width = t.width, height = t.height;
@@ -680,14 +682,22 @@ GDEV XYZA texture_color(const DevScene& S, const DevTexture& t, double u, double
     const double* cc = ((ut + vt) % 2 == 0) ? t.c1 : t.c2;
     c = XYZA{cc[0], cc[1], cc[2], cc[3]};
   } else {
-    c = sample_blackbody(S, temperature * redshift);
+    c = sample_blackbody_lut(bb_lt, bb_xyz, S.bb_n, temperature * redshift);
   }
-  double f = rpow(redshift, t.beaming);  // apply_beaming (color.rs:72-80)
+  // apply_beaming (color.rs:72-80): powf(redshift, e); pow(x, +-0) is 1 for every x (C99
+  // F.9.4.4, glibc), so the stock scenes' exponent 0 skips the call
+  double f = t.beaming == 0.0 ? 1.0 : rpow(redshift, t.beaming);
   return XYZA{c.x * f, c.y * f, c.z * f, c.a};
 }
+GDEV XYZA texture_color(const DevScene& S, const DevTexture& t, double u, double v, double redshift,
+                        double temperature) {
+  return texture_color_lut(S, t, u, v, redshift, temperature, S.bb_log_t, S.bb_xyz);
+}
 
-// KerrTemperatureComputer::compute_temperature (temperature.rs:198-253)
-GDEV int compute_temperature(const DevObject& o, double radius, double* out) {
+// KerrTemperatureComputer::compute_temperature (temperature.rs:198-253); lut_r / lut_t:
+// the object's (r, T) table in global memory or an LDS copy
+GDEV int compute_temperature_lut(const DevObject& o, const double* lut_r, const double* lut_t, double radius,
+                                 double* out) {
   if (o.temp_kind == GRT_TEMP_CONSTANT) {
     *out = o.temp_constant;
     return GRT_OK;
@@ -695,18 +705,21 @@ GDEV int compute_temperature(const DevObject& o, double radius, double* out) {
   if (!isfinite(radius)) return GRT_ERR_NON_FINITE_RADIUS;
   if (radius < o.r_isco) return GRT_ERR_BELOW_RISCO;
   uint32_t n = o.lut_n;
-  if (radius <= o.lut_r[0]) { *out = o.lut_t[0]; return GRT_OK; }
-  if (radius >= o.lut_r[n - 1]) { *out = o.lut_t[n - 1]; return GRT_OK; }
+  if (radius <= lut_r[0]) { *out = lut_t[0]; return GRT_OK; }
+  if (radius >= lut_r[n - 1]) { *out = lut_t[n - 1]; return GRT_OK; }
   uint32_t lo = 0, hi = n;
   while (lo < hi) {
     uint32_t mid = lo + (hi - lo) / 2;
-    if (o.lut_r[mid] <= radius) lo = mid + 1; else hi = mid;
+    if (lut_r[mid] <= radius) lo = mid + 1; else hi = mid;
   }
   uint32_t idx = lo == 0 ? 0 : lo - 1;
-  double r0 = o.lut_r[idx], t0 = o.lut_t[idx], r1 = o.lut_r[idx + 1], t1 = o.lut_t[idx + 1];
+  double r0 = lut_r[idx], t0 = lut_t[idx], r1 = lut_r[idx + 1], t1 = lut_t[idx + 1];
   double t = (radius - r0) / (r1 - r0);
   *out = t0 + t * (t1 - t0);
   return GRT_OK;
+}
+GDEV int compute_temperature(const DevObject& o, double radius, double* out) {
+  return compute_temperature_lut(o, o.lut_r, o.lut_t, radius, out);
 }
 
 #include "volumetric.h"

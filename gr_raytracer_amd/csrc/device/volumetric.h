@@ -204,7 +204,14 @@ GDEV double perlin3(const uint8_t* P, double px, double py, double pz) {
 }
 
 // ---- density, uv (volumetric_disc.rs:97-152) -------------------------------------
-GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p) {
+// Also returns the in-plane coordinates (x_local, y_local) and sin / cos of their angle
+// phi when the noise was evaluated (*noise): get_uv (:140-152) recomputes exactly these
+// values at the same point, so the raymarch reuses them.
+struct PlaneAngle {
+  double x, y, sp, cp;
+};
+GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p, PlaneAngle* pa, bool* noise) {
+  *noise = false;
   const V3 ax = vaxis(o);
   const double h = fabs(vdot(p, ax));
   const double r = vnorm(vcross(p, ax));
@@ -218,9 +225,12 @@ GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p) {
   boundary_falloff *= glibc::exp_(-1.0 / fmax(d1 * d1, 0.0001));
   boundary_falloff *= glibc::exp_(-1.0 / fmax(d2 * d2, 0.0001));
   const V3 e1{o.e1[0], o.e1[1], o.e1[2]}, e2{o.e2[0], o.e2[1], o.e2[2]};
-  const double phi = atan2(vdot(p, e2), vdot(p, e1));
+  const double x_local = vdot(p, e1), y_local = vdot(p, e2);
+  const double phi = atan2(y_local, x_local);
   double sp, cp;
   rsincos(phi, &sp, &cp);
+  *noise = true;
+  *pa = PlaneAngle{x_local, y_local, sp, cp};
   const double npx = r * o.ns[0], npy = cp * o.ns[1], npz = sp * o.ns[1];
   double n = 0.0, frequency = 4.0, amplitude = 1.0;  // fbm (:330-342)
   for (uint32_t i = 0; i < o.octaves; ++i) {
@@ -233,16 +243,12 @@ GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p) {
   return n2 * radial_base * vertical_falloff * boundary_falloff;
 }
 
-GDEV void vdisc_uv(const DevObject& o, const V3& p, double* u, double* v) {
-  const V3 e1{o.e1[0], o.e1[1], o.e1[2]}, e2{o.e2[0], o.e2[1], o.e2[2]};
-  const double x = vdot(p, e1), y = vdot(p, e2);
-  const double rr = sqrt(x * x + y * y);
-  const double phi = atan2(y, x);
+// get_uv from the density's PlaneAngle (same point: the same x, y, phi, sin, cos)
+GDEV void vdisc_uv(const DevObject& o, const PlaneAngle& pa, double* u, double* v) {
+  const double rr = sqrt(pa.x * pa.x + pa.y * pa.y);
   const double r = (rr - o.rin) / (o.rout - o.rin);
-  double sp, cp;
-  rsincos(phi, &sp, &cp);
-  *u = 0.5 + 0.5 * r * cp;
-  *v = 0.5 + 0.5 * r * sp;
+  *u = 0.5 + 0.5 * r * pa.cp;
+  *v = 0.5 + 0.5 * r * pa.sp;
 }
 
 // precompute_exit_distance (:172-196): distance to the first boundary crossing (t > 1e-9)
@@ -281,11 +287,35 @@ GDEV bool killing_at(const DevScene& S, const V3& p, double* ut, double* uphi) {
 
 // ---- march kernel: one lane per job, refilled by wave ballot -----------------------
 // Job = (ray slot << 8) | candidate slot.  Colour goes to ws.vcol at the candidate slot.
+// The per-sample table lookups (temperature LUT of the first volumetric object with one,
+// the blackbody LUT) are binary searches of ~10 dependent loads: staged in LDS (48 KB).
+constexpr uint32_t MARCH_LUT_MAX = 1000;
 template <int G>
 __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restrict__ Sp, Workspace ws) {
   const DevScene& S = *Sp;
   __shared__ uint8_t lds_perm[GRT_MAX_OBJECTS * 256];
+  __shared__ double lds_tr[MARCH_LUT_MAX], lds_tt[MARCH_LUT_MAX];
+  __shared__ double lds_bt[MARCH_LUT_MAX], lds_bx[3 * MARCH_LUT_MAX];
   for (unsigned i = threadIdx.x; i < GRT_MAX_OBJECTS * 256u; i += blockDim.x) lds_perm[i] = S.perm[i >> 8][i & 255u];
+  int lut_obj = -1;  // wave-uniform
+  for (uint32_t q = 0; q < S.n_objects; ++q)
+    if (lut_obj < 0 && S.obj[q].kind == GRT_OBJ_VOLUMETRIC_DISC && S.obj[q].temp_kind == GRT_TEMP_KERR_LUT &&
+        S.obj[q].lut_n <= MARCH_LUT_MAX)
+      lut_obj = (int)q;
+  if (lut_obj >= 0) {
+    const DevObject& lo = S.obj[lut_obj];
+    for (unsigned i = threadIdx.x; i < lo.lut_n; i += blockDim.x) {
+      lds_tr[i] = lo.lut_r[i];
+      lds_tt[i] = lo.lut_t[i];
+    }
+  }
+  const bool bb_lds = S.bb_n >= 2 && S.bb_n <= MARCH_LUT_MAX;
+  if (bb_lds) {
+    for (unsigned i = threadIdx.x; i < S.bb_n; i += blockDim.x) lds_bt[i] = S.bb_log_t[i];
+    for (unsigned i = threadIdx.x; i < 3u * S.bb_n; i += blockDim.x) lds_bx[i] = S.bb_xyz[i];
+  }
+  const double* bb_lt = bb_lds ? lds_bt : S.bb_log_t;
+  const double* bb_xyz = bb_lds ? lds_bx : S.bb_xyz;
   glibc::tables_to_lds();  // includes the block barrier
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -297,7 +327,7 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
   uint64_t chunk_next = 0, chunk_end = 0;
   bool active = false, done = false;
   // lane state
-  uint64_t slot = 0, i = 0, n_samples = 0;
+  uint64_t slot = 0, i = 0, n_samples = 0, n_noise = 0, n_emit = 0;
   uint32_t k = 0;
   V3 ro{0, 0, 0}, rd{0, 0, 0};
   double d_o = 0.0, exit_d = 0.0, transparency = 1.0, aws = 0.0, awt = 0.0;
@@ -361,7 +391,10 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
     d_o += d_s;
     n_samples++;
     bool failed = false;
-    const double density = vdisc_density(o, P, p);
+    PlaneAngle pa;
+    bool noise;
+    const double density = vdisc_density(o, P, p, &pa, &noise);
+    n_noise += noise ? 1u : 0u;
     if (density > 0.0) {
       const double sig = o.sig_a + o.sig_s;
       transparency *= glibc::exp_(-d_s * density * sig);
@@ -371,12 +404,15 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
         const double redshift = obs / emitter_energy;
         const double r_dist = vnorm(vcross(p, vaxis(o)));
         double temperature;
-        if (compute_temperature(o, r_dist, &temperature) != GRT_OK) {
+        const bool lds_t = (int)k == lut_obj;
+        if (compute_temperature_lut(o, lds_t ? lds_tr : o.lut_r, lds_t ? lds_tt : o.lut_t, r_dist, &temperature) !=
+            GRT_OK) {
           failed = true;  // Err -> color_at_uv's unwrap_or_else: (0, 0, 0, 0)
         } else {
+          n_emit++;
           double u, v;
-          vdisc_uv(o, p, &u, &v);
-          const XYZA light = texture_color(S, o.tex, u, v, redshift, temperature);
+          vdisc_uv(o, pa, &u, &v);
+          const XYZA light = texture_color_lut(S, o.tex, u, v, redshift, temperature, bb_lt, bb_xyz);
           const double light_attenuation = glibc::exp_(-density * d_s * sig);
           const double ratio = temperature / o.bref;
           const double r2 = ratio * ratio;
@@ -421,6 +457,14 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
     }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) n_samples += __shfl_down(n_samples, off);
-  if (lane == 0) atomicAdd(ws.march + 2, (unsigned long long)n_samples);
+  for (int off = 32; off > 0; off >>= 1) {
+    n_samples += __shfl_down(n_samples, off);
+    n_noise += __shfl_down(n_noise, off);
+    n_emit += __shfl_down(n_emit, off);
+  }
+  if (lane == 0) {
+    atomicAdd(ws.march + 2, (unsigned long long)n_samples);
+    atomicAdd(ws.march + 4, (unsigned long long)n_noise);
+    atomicAdd(ws.march + 5, (unsigned long long)n_emit);
+  }
 }

@@ -121,7 +121,8 @@ class RenderResult:
 def _stats_dict(st: L.Stats) -> dict:
     return {"accepted_steps": int(st.accepted_steps), "attempts": int(st.attempts), "rays": int(st.rays),
             "hit_overflows": int(st.hit_overflows), "kernel_ms": float(st.kernel_ms),
-            "march_jobs": int(st.march_jobs), "march_samples": int(st.march_samples)}
+            "march_jobs": int(st.march_jobs), "march_samples": int(st.march_samples),
+            "march_noise_samples": int(st.march_noise_samples), "march_emit_samples": int(st.march_emit_samples)}
 
 
 class Scene:

@@ -310,6 +310,8 @@ typedef struct grt_stats {
    * volumetric intersection whose colour reaches the composite, and their samples. */
   uint64_t march_jobs;
   uint64_t march_samples;
+  uint64_t march_noise_samples; /* samples inside the density's support (fBm evaluated) */
+  uint64_t march_emit_samples;  /* samples with density > 0 that emitted                */
 } grt_stats;
 
 /* Optional per-sample sub-pixel offsets (get_ray_for_offset, camera.rs:247-254):
