@@ -410,5 +410,63 @@ GRT_GLIBC_FN bool sincos_fast(double x, double* sinx, double* cosx) {
   return false;
 }
 
+// sincos_fast without the region branches, for angles spread over (-pi, pi] within a
+// wave (the VolumetricDisc's in-plane angle): every region of sincos_fast evaluates one
+// do_sin_nf and one do_cos_nf, so the arguments are selected per lane, both are
+// evaluated once (do_sin_nf's Taylor branch as a select too), and the results are
+// routed and signed per region.  The same operations on the same operands as
+// sincos_fast, hence the same bits (tests/test_glibc_math.py).
+GRT_GLIBC_FN double do_sin_nf_sel(double x, double dx) {
+  const double taylor = taylor_sin_nf(x, dx);
+  if (x <= 0.0) dx = -dx;
+  const double u = BIG + fabs_(x);
+  const double xr = fabs_(x) - (u - BIG);
+  const int k = (int)((uint32_t)as_u64(u) << 2);  // |x| < 0.855469 in every region: in the table
+  const double sn = GRT_SINCOS(k), ssn = GRT_SINCOS(k + 1), cs = GRT_SINCOS(k + 2), ccs = GRT_SINCOS(k + 3);
+  const double xx = xr * xr;
+  const double s = xr + (dx + xr * xx * (SN3 + xx * SN5));
+  const double c = xr * dx + xx * (CS2 + xx * (CS4 + xx * CS6));
+  const double cor = (ssn + s * ccs - sn * c) + cs * s;
+  return fabs_(x) < TAYLOR_MAX ? taylor : copysign_(sn + cor, x);
+}
+
+GRT_GLIBC_FN bool sincos_fast_uniform(double x, double* sinx, double* cosx) {
+  const uint32_t k = (uint32_t)(as_u64(x) >> 32) & 0x7fffffffu;
+  if (k >= 0x419921fbu) return false;
+  const bool ra = k < 0x3feb6000u;                    // |x| < 0.855469: do_sin(x, 0), do_cos(x, 0)
+  const bool rb = !ra && k < 0x400368fdu;             // |x| < 2.426265: pi/2 - |x| forms
+  const double y = HP0 - fabs_(x);                    // region B
+  const double ab = y + HP1;
+  const double dab = (y - ab) + HP1;
+  double ac, dac;                                     // region C: x = n pi/2 + (a + da)
+  const int n = reduce_sincos_nf(x, &ac, &dac);
+  const double s_x = ra ? x : (rb ? ab : ac);
+  const double s_dx = ra ? 0.0 : (rb ? dab : dac);
+  const double c_x = ra ? x : (rb ? y : ac);
+  const double c_dx = ra ? 0.0 : (rb ? HP1 : dac);
+  const double DS = do_sin_nf_sel(s_x, s_dx);
+  const double DC = do_cos_nf(c_x, c_dx);
+  double s, c;
+  if (ra) {
+    s = DS;
+    c = DC;
+  } else if (rb) {
+    s = copysign_(DC, x);
+    c = DS;
+  } else {  // do_sincos_nf(a, da, n) and (.., n + 1)
+    const double rs = (n & 1) ? DC : DS;
+    const double rc = (n & 1) ? DS : DC;
+    s = (n & 2) ? -rs : rs;
+    c = ((n + 1) & 2) ? -rc : rc;
+  }
+  if (k < 0x3e400000u) {
+    s = x;
+    c = 1.0;
+  }
+  *sinx = s;
+  *cosx = c;
+  return true;
+}
+
 }  // namespace glibc
 }  // namespace grt

@@ -172,13 +172,17 @@ GDEV double grad_dot(uint32_t h, double x, double y, double z) {
 }
 GDEV double s_curve5(double x) { return x * x * x * (x * (x * 6.0 - 15.0) + 10.0); }
 
+// (corner as isize) & 0xff of an integral double: fl - 256 floor(fl / 256) is exact
+// (power-of-two scaling, integral operands below 2^53) and lies in [0, 255]; the
+// reference's numcast() panics beyond the isize range, where this is never reached.
+GDEV uint32_t lattice_byte(double fl) { return (uint32_t)(int32_t)__builtin_fma(-256.0, floor(fl * 0.00390625), fl); }
+
 GDEV double perlin3(const uint8_t* P, double px, double py, double pz) {
   const double fx = floor(px), fy = floor(py), fz = floor(pz);
-  const int64_t cx = (int64_t)fx, cy = (int64_t)fy, cz = (int64_t)fz;
   const double dx = px - fx, dy = py - fy, dz = pz - fz;
-  const uint32_t x0 = (uint32_t)(cx & 0xff), x1 = (uint32_t)((cx + 1) & 0xff);
-  const uint32_t y0 = (uint32_t)(cy & 0xff), y1 = (uint32_t)((cy + 1) & 0xff);
-  const uint32_t z0 = (uint32_t)(cz & 0xff), z1 = (uint32_t)((cz + 1) & 0xff);
+  const uint32_t x0 = lattice_byte(fx), x1 = (x0 + 1u) & 0xffu;
+  const uint32_t y0 = lattice_byte(fy), y1 = (y0 + 1u) & 0xffu;
+  const uint32_t z0 = lattice_byte(fz), z1 = (z0 + 1u) & 0xffu;
   const uint32_t a0 = P[x0], a1 = P[x1];
   const uint32_t b00 = P[a0 ^ y0], b10 = P[a1 ^ y0], b01 = P[a0 ^ y1], b11 = P[a1 ^ y1];
   const double dx1 = dx - 1.0, dy1 = dy - 1.0, dz1 = dz - 1.0;
@@ -227,8 +231,8 @@ GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p, Pla
   const V3 e1{o.e1[0], o.e1[1], o.e1[2]}, e2{o.e2[0], o.e2[1], o.e2[2]};
   const double x_local = vdot(p, e1), y_local = vdot(p, e2);
   const double phi = atan2(y_local, x_local);
-  double sp, cp;
-  rsincos(phi, &sp, &cp);
+  double sp, cp;  // phi is spread over (-pi, pi] within a wave: the branch-free sincos
+  if (!glibc::sincos_fast_uniform(phi, &sp, &cp)) sincos(phi, &sp, &cp);
   *noise = true;
   *pa = PlaneAngle{x_local, y_local, sp, cp};
   const double npx = r * o.ns[0], npy = cp * o.ns[1], npz = sp * o.ns[1];

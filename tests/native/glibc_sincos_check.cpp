@@ -22,14 +22,18 @@ int main(int argc, char** argv) {
       case 1: x = (u01(rng) - 0.5) * 40.0; break;
       case 2: x = std::ldexp(u01(rng) - 0.5, (int)(rng() % 60) - 40); break;
       case 3: x = 1.5707963267948966 + (u01(rng) - 0.5) * 1e-6; break;
+      case 5: x = (u01(rng) * 2.0 - 1.0) * 3.141592653589793; break;  // VolumetricDisc phi
       default: x = (u01(rng) - 0.5) * 2e8;
     }
-    double gs, gc, ws, wc;
+    double gs, gc, ws, wc, us, uc;
     if (!grt::glibc::sincos_fast(x, &gs, &gc)) continue;
     ++fast;
     sincos(x, &ws, &wc);
-    if (memcmp(&gs, &ws, 8) != 0 || memcmp(&gc, &wc, 8) != 0) {
-      if (bad < 5) printf("# mismatch x=%a got=(%a,%a) want=(%a,%a)\n", x, gs, gc, ws, wc);
+    // the branch-free variant must return the same bits on the same domain
+    const bool uok = grt::glibc::sincos_fast_uniform(x, &us, &uc);
+    if (memcmp(&gs, &ws, 8) != 0 || memcmp(&gc, &wc, 8) != 0 || !uok || memcmp(&us, &ws, 8) != 0 ||
+        memcmp(&uc, &wc, 8) != 0) {
+      if (bad < 5) printf("# mismatch x=%a got=(%a,%a) uniform=(%a,%a) want=(%a,%a)\n", x, gs, gc, us, uc, ws, wc);
       ++bad;
     }
   }

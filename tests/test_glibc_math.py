@@ -41,7 +41,7 @@ def test_tables_match_the_installed_libm():
 
 
 TRIG_MODES = {0: "ray theta", 1: "several periods", 2: "magnitudes 2^-41..2^19", 3: "near pi/2",
-              4: "up to the reduction limit"}
+              4: "up to the reduction limit", 5: "(-pi, pi): VolumetricDisc phi"}
 
 
 def _build(tmp_path_factory, name, extra=()):
@@ -60,8 +60,9 @@ def trig_checkers(tmp_path_factory):
 
 @pytest.mark.parametrize("mode", sorted(TRIG_MODES))
 def test_device_sin_cos_sincos_are_bit_identical_to_glibc(trig_checkers, mode):
-    """sin_fast / cos_fast == glibc sin / cos (FMA ifunc builds); sincos_fast == glibc
-    sincos (baseline build), on |x| < 105414350."""
+    """sin_fast / cos_fast == glibc sin / cos (FMA ifunc builds); sincos_fast and its
+    branch-free variant sincos_fast_uniform == glibc sincos (baseline build), on
+    |x| < 105414350."""
     for exe in trig_checkers:
         out = subprocess.run([str(exe), str(mode), "300000"], check=True, capture_output=True, text=True).stdout
         n, fast, bad = map(int, out.strip().splitlines()[-1].split())

@@ -54,7 +54,7 @@ def test_volumetric_scene_crops(grt, oracle, gpu, toml, rect):
 def test_kerr_schild_volumetric_crop(grt, oracle, gpu):
     """kerr-volumetric-stony.toml (Kerr-Schild chart, Cartesian: no far-field filter)."""
     hs = vol_host_scene(grt, "kerr-volumetric-stony.toml", 160)
-    got, _ = compare(grt, oracle, hs, (76, 10, 8, 24))
+    got, _ = compare(grt, oracle, hs, (76, 10, 8, 24), max_sensitive=0.05)  # KS: chaotic edge pixels
     assert got.stats["march_jobs"] > 0
 
 

@@ -39,7 +39,8 @@ def main():
         st = r.stats
         print(json.dumps({"scene": name, "pixels": width * width, "kernel_ms": st["kernel_ms"], "wall_s": wall,
                           "accepted_steps": st["accepted_steps"], "march_jobs": st["march_jobs"],
-                          "march_samples": st["march_samples"],
+                          "march_samples": st["march_samples"], "march_noise_samples": st["march_noise_samples"],
+                          "march_emit_samples": st["march_emit_samples"],
                           "hit_pixels": int((r.ray_class == 2).sum()),
                           "march_samples_per_s": st["march_samples"] / (st["kernel_ms"] * 1e-3)}), flush=True)
 
