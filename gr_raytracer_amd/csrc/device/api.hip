@@ -298,6 +298,7 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
       q.vol_far_r = 2.0 * corner * (1.0 + 1e-6);
       q.vol_rmax = 1e6 * q.cap_h;
       q.vol_slab_h = q.cap_h * (1.0 + 1e-6) + 1e-12;
+      q.vol_h_cut = std::sqrt(std::log(1000.0)) * o.thickness * (1.0 + 1e-6);  // exp(-(h/th)^2) < 0.001 beyond
       q.vol_slab_ok = (q.ax[0] == 0.0 && q.ax[1] == 0.0 && q.ax[2] == 1.0) ? 1 : 0;
       if (!std::isfinite(q.vol_far_r) || !std::isfinite(q.vol_rmax) || !(q.cap_h > 0.0)) {
         q.vol_far_r = HUGE_VAL;

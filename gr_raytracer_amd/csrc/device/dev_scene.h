@@ -46,6 +46,7 @@ struct DevObject {
   // vol_far_r = 2 * |capture corner| * (1 + 1e-6); vol_rmax bounds the radii it is
   // used at; vol_slab_h = cap_h * (1 + 1e-6) + 1e-12 (axis == z only, vol_slab_ok)
   double vol_far_r, vol_rmax, vol_slab_h;
+  double vol_h_cut;            // |h| beyond which the vertical falloff is < 0.001: 2.62826 thickness (1 + 1e-6)
   int32_t vol_slab_ok, _pad2;
 };
 

@@ -289,6 +289,31 @@ GDEV bool killing_at(const DevScene& S, const V3& p, double* ut, double* uphi) {
   }
 }
 
+// True when no sample at or beyond p (along rd) can have density > 0, so the rest of
+// the raymarch adds nothing: the colour is final whatever the exit test or max_steps
+// would decide later.  Density needs rin < |p x axis| < rout and a vertical falloff
+// exp(-(h/thickness)^2) >= 0.001, i.e. |h| <= 2.62826 thickness (vol_h_cut carries a
+// 1e-6 margin).  h is linear along the ray and |p x axis|^2 convex, so a sample beyond
+// the cut that moves away from the mid-plane, or beyond rout that moves outward, stays
+// outside.  The margins (1e-9 relative, 1e-9 absolute) exceed the rounding of the
+// positions any later sample could compute (|p| <= |ro| + max_steps * step_size) by
+// orders of magnitude; slopes within -1e-15 of zero count as non-approaching, which
+// moves h or r^2 by < 1e-12 over the whole march.
+//   Most raymarch jobs start where a window LEAVES the capture region (volumetric_
+// disc.rs:540-548 returns that crossing too): they march outward through empty space
+// for up to max_steps samples, and end on the first sample here.
+GDEV bool vdisc_no_more_density(const DevObject& o, const V3& p, const V3& rd) {
+  const V3 ax = vaxis(o);
+  const double pn = fabs(p.x) + fabs(p.y) + fabs(p.z);
+  const double tol = 1e-9 * (1.0 + pn + o.m_maxdist);
+  const double h = vdot(p, ax), s = vdot(rd, ax);
+  if (fabs(h) > o.vol_h_cut + tol && (h > 0.0 ? s : -s) >= -1e-15) return true;
+  const V3 c = vcross(p, ax), cd = vcross(rd, ax);
+  const double r2 = vdot(c, c);
+  const double rmin = o.rout + tol;
+  return r2 > rmin * rmin && vdot(c, cd) >= -1e-15 * (1.0 + pn);
+}
+
 // ---- march kernel: one lane per job, refilled by wave ballot -----------------------
 // Job = (ray slot << 8) | candidate slot.  Colour goes to ws.vcol at the candidate slot.
 // The per-sample table lookups (temperature LUT of the first volumetric object with one,
@@ -432,7 +457,7 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
         }
       }
     }
-    bool finished = failed;
+    bool finished = failed || (density == 0.0 && vdisc_no_more_density(o, p, rd));
     if (!finished) {
       bool exited;
       if (cached) {

@@ -14,14 +14,16 @@ is pinned by the reference's volumetric_disc.rs tests (tests/test_volumetric.py)
 import numpy as np
 import pytest
 
-from conftest import RESOURCES, SCENES, c2_opts, c3_opts
+from conftest import RESOURCES, SCENES, c2_opts, c3_opts, c4_opts
 from test_gpu_parity import check_parity, gpu_scene, oracle_pair
 
 pytestmark = pytest.mark.gpu
 
 
 def vol_host_scene(grt, toml, width, height=None, path=None):
-    opts = (c3_opts if toml.startswith("kerr") else c2_opts)(grt, width=width, height=height or width)
+    # the reference's example cameras: C2's (Schwarzschild), C3's (KerrBL), C4's (Kerr-Schild)
+    mk = c4_opts if toml.startswith("kerr-volumetric") else (c3_opts if toml.startswith("kerr") else c2_opts)
+    opts = mk(grt, width=width, height=height or width)
     return grt.HostScene(str(path or (SCENES / toml)), opts, str(RESOURCES))
 
 
@@ -54,7 +56,7 @@ def test_volumetric_scene_crops(grt, oracle, gpu, toml, rect):
 def test_kerr_schild_volumetric_crop(grt, oracle, gpu):
     """kerr-volumetric-stony.toml (Kerr-Schild chart, Cartesian: no far-field filter)."""
     hs = vol_host_scene(grt, "kerr-volumetric-stony.toml", 160)
-    got, _ = compare(grt, oracle, hs, (76, 10, 8, 24), max_sensitive=0.05)  # KS: chaotic edge pixels
+    got, _ = compare(grt, oracle, hs, (76, 0, 6, 40), max_sensitive=0.05)  # KS: chaotic edge pixels
     assert got.stats["march_jobs"] > 0
 
 

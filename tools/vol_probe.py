@@ -14,12 +14,14 @@ import numpy as np  # noqa: E402
 
 import gr_raytracer_amd as g  # noqa: E402
 import pyoracle as O  # noqa: E402
-from conftest import c2_opts, c3_opts, host_scene  # noqa: E402
+from conftest import c2_opts, c3_opts, c4_opts, host_scene  # noqa: E402
 
 
 def main():
     toml, W = sys.argv[1], int(sys.argv[2])
-    opts = (c3_opts if "kerr" in toml else c2_opts)(g, width=W, height=W)
+    # C2 camera for Schwarzschild, C3's for KerrBL, C4's for Kerr-Schild (as the reference's examples)
+    mk = c4_opts if toml.startswith("kerr-") and not toml.startswith("kerr-bl") else (c3_opts if "kerr" in toml else c2_opts)
+    opts = mk(g, width=W, height=W)
     hs = host_scene(g, toml, opts)
     t = time.time()
     r = O.render_pixels(hs.desc, 0, 0, W, W, threads=8)
