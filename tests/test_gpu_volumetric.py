@@ -54,10 +54,25 @@ def test_volumetric_scene_crops(grt, oracle, gpu, toml, rect):
 
 
 def test_kerr_schild_volumetric_crop(grt, oracle, gpu):
-    """kerr-volumetric-stony.toml (Kerr-Schild chart, Cartesian: no far-field filter)."""
+    """kerr-volumetric-stony.toml (Kerr-Schild chart, Cartesian: no far-field filter).
+
+    Here the oracle's own last-ulp probes move most pixels (measured: 185 of 240): the
+    finite-difference metric derivatives make the step controller's accept / reject
+    decisions sensitive to the last ulp, a changed step sequence moves the window chord
+    that crosses the gas's capture boundary, and the fBm (up to 512 x 25 cycles per unit)
+    turns that shift into a different colour.  The GPU integrates Kerr-Schild bit for bit
+    like the oracle (glibc-exact pow; no trig on this chart), so it is held to the oracle
+    itself: 95% of the pixels within 1e-4 with identical class."""
+    from test_gpu_parity import agree
+
     hs = vol_host_scene(grt, "kerr-volumetric-stony.toml", 160)
-    got, _ = compare(grt, oracle, hs, (76, 0, 6, 40), max_sensitive=0.05)  # KS: chaotic edge pixels
-    assert got.stats["march_jobs"] > 0
+    rect = (76, 0, 6, 40)
+    got = gpu_scene(grt, hs).render_pixels(*rect)
+    ref = oracle.render_pixels(hs.desc, *rect, threads=16)
+    ok = agree(got.xyza64, got.ray_class, ref)
+    assert ok.mean() >= 0.95, (ok.mean(), np.where(~ok)[0][:10])
+    assert np.array_equal(got.status, ref["status"]) and np.mean(got.steps == ref["steps"]) >= 0.95
+    assert got.stats["march_jobs"] > 0 and np.any(got.ray_class == 2)
 
 
 FLAT = """celestial_temperature = 0.0
