@@ -303,6 +303,10 @@ int main(int argc, char** argv) {
                "(%.3e steps/s)\n",
                (unsigned long long)st.rays, (unsigned long long)st.accepted_steps, (unsigned long long)st.attempts,
                (unsigned long long)nsel, st.kernel_ms, st.accepted_steps / (st.kernel_ms * 1e-3));
+  if (st.march_jobs)
+    std::fprintf(stderr, "[grt] VolumetricDisc: %llu raymarches, %llu samples (%llu with noise, %llu emitting)\n",
+                 (unsigned long long)st.march_jobs, (unsigned long long)st.march_samples,
+                 (unsigned long long)st.march_noise_samples, (unsigned long long)st.march_emit_samples);
   std::string err;
   bool ok;
   if (filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".hdr") == 0) {

@@ -149,3 +149,27 @@ def test_volumetric_adaptive_section(grt, oracle, gpu):
     assert nsel == ref_nsel and nsel > 0 and st["march_jobs"] > 0
     ok = np.all(np.abs(out - ref) <= 1e-4 * np.maximum(np.abs(ref), 1e-6), axis=1)
     assert ok.mean() >= 0.98, ok.mean()
+
+
+def test_cli_renders_a_stock_volumetric_scene(grt, oracle, gpu, tmp_path):
+    """`grt ... --config-file=schwarzschild-volumetric-stony.toml render` (stock TOML:
+    adaptive 4x4 on): the raw f64 frame is grt_render_section's, the PNG its reference
+    output stage."""
+    import subprocess
+    from pathlib import Path
+
+    Image = pytest.importorskip("PIL.Image")
+    root = Path(__file__).resolve().parents[1]
+    png, raw = tmp_path / "vol.png", tmp_path / "vol.raw"
+    toml = SCENES / "schwarzschild-volumetric-stony.toml"
+    subprocess.run([str(root / "gr_raytracer_amd" / "lib" / "grt"), "--width=48", "--height=40",
+                    "--camera-position=-16.0,0.0,3.5", "--theta=-3.142", "--max-steps=100000",
+                    f"--config-file={toml}", f"--resource-root={RESOURCES}", "render", f"--filename={png}",
+                    f"--raw-out={raw}", f"--device={gpu}"], check=True, timeout=300)
+    x = np.fromfile(raw, np.float64).reshape(-1, 4)
+    hs = grt.HostScene(str(toml), c2_opts(grt, width=48, height=40), str(RESOURCES))
+    sc = gpu_scene(grt, hs)
+    out, cls, nsel, st = sc.render_section()
+    assert np.array_equal(x, out) and nsel > 0 and st["march_jobs"] > 0
+    img = np.asarray(Image.open(png).convert("RGB")).reshape(-1, 3)
+    assert np.array_equal(img, oracle.xyz_to_srgb8(x, 0))
