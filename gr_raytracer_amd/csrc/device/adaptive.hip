@@ -18,13 +18,14 @@
 
 namespace grt {
 
-__device__ __forceinline__ bool pair_triggers(const double* p, int pc, const double* q, int qc,
+// should_supersample_pair (:91-108) on the luminance Y and opacity alpha of two pixels
+__device__ __forceinline__ bool pair_triggers(double py, double pa, int pc, double qy, double qa, int qc,
                                               const AdaptiveParams& a) {
   if (pc != qc) return true;
   if (a.exclude_background_contrast && pc == GRT_CLASS_ESCAPED) return false;
-  bool visible = fmax(p[1], q[1]) > a.min_lum;
-  double lc = fabs(p[1] - q[1]) / (p[1] + q[1] + 1e-4);
-  double oc = fabs(p[3] - q[3]);
+  bool visible = fmax(py, qy) > a.min_lum;
+  double lc = fabs(py - qy) / (py + qy + 1e-4);
+  double oc = fabs(pa - qa);
   return visible && (lc > a.luminance_contrast_threshold || oc > a.opacity_contrast_threshold);
 }
 
@@ -42,7 +43,35 @@ __global__ void select_kernel(const double* __restrict__ xyza, const uint8_t* __
     int nr = row + sh[s][0], nc = col + sh[s][1];
     if (nr < 0 || nr >= (int)a.h || nc < 0 || nc >= (int)a.w) continue;
     uint64_t j = (uint64_t)nr * a.w + nc;
-    if (pair_triggers(p, pc, xyza + 4 * j, cls[j], a)) {
+    if (pair_triggers(p[1], p[3], pc, xyza[4 * j + 1], xyza[4 * j + 3], cls[j], a)) {
+      f = 1;
+      break;
+    }
+  }
+  flags[i] = f;
+}
+
+// The same stencil for the local pixels of one row-band shard (grt_row_shard) of a
+// frame whose 1-spp luminance / opacity and class are known frame-wide: ya holds
+// (Y, alpha) per frame pixel, cls the class, both in frame order (the allgather of the
+// multi-GPU adaptive pass).  a.w x a.h is the frame; neighbours outside
+// it are skipped exactly as outside a single-process section.  flags: local order.
+__global__ void select_shard_kernel(const double* __restrict__ ya, const uint8_t* __restrict__ cls,
+                                    AdaptiveParams a, uint32_t band_rows, uint32_t shard, uint32_t n_shards,
+                                    uint32_t local_rows, uint8_t* __restrict__ flags) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)local_rows * a.w) return;
+  int row = (int)shard_frame_row(band_rows, shard, n_shards, (uint32_t)(i / a.w)), col = (int)(i % a.w);
+  const int sh[8][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 1}, {1, -1}, {1, 0}, {1, 1}};
+  uint64_t c = (uint64_t)row * a.w + col;
+  double py = ya[2 * c], pa = ya[2 * c + 1];
+  int pc = cls[c];
+  uint8_t f = 0;
+  for (int s = 0; s < 8; ++s) {
+    int nr = row + sh[s][0], nc = col + sh[s][1];
+    if (nr < 0 || nr >= (int)a.h || nc < 0 || nc >= (int)a.w) continue;
+    uint64_t j = (uint64_t)nr * a.w + nc;
+    if (pair_triggers(py, pa, pc, ya[2 * j], ya[2 * j + 1], cls[j], a)) {
       f = 1;
       break;
     }
@@ -122,6 +151,15 @@ hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const Ada
   uint64_t n = (uint64_t)p.w * p.h;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(select_kernel, dim3(nblocks(n, 256)), dim3(256), 0, stream, d_xyza64, d_cls, p, d_flags);
+  return hipGetLastError();
+}
+hipError_t launch_select_shard(const double* d_ya, const uint8_t* d_cls, const AdaptiveParams& p, uint32_t band_rows,
+                               uint32_t shard, uint32_t n_shards, uint32_t local_rows, uint8_t* d_flags,
+                               hipStream_t stream) {
+  uint64_t n = (uint64_t)local_rows * p.w;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(select_shard_kernel, dim3(nblocks(n, 256)), dim3(256), 0, stream, d_ya, d_cls, p, band_rows,
+                     shard, n_shards, local_rows, d_flags);
   return hipGetLastError();
 }
 hipError_t launch_make_offsets(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, uint32_t row0,

@@ -717,6 +717,28 @@ int grt_trace_rays(grt_scene* s, int device, uint64_t n, const double* positions
                       status_out);
 }
 
+// resolve_minimum_luminance's relative floor (raytracer.rs:118-129): 1e-3 x the element
+// at ((n - 1) * 0.99) as usize in f64::total_cmp order (select_nth_unstable_by selects
+// the same element as nth_element under the same total order).  Reorders `lum`.
+static double relative_min_luminance(std::vector<double>& lum) {
+  if (lum.empty()) return 0.0;
+  uint64_t index = (uint64_t)((double)(lum.size() - 1) * 0.99);
+  auto key = [](double v) {
+    int64_t b;
+    std::memcpy(&b, &v, 8);
+    return b ^ (int64_t)((uint64_t)(b >> 63) >> 1);
+  };
+  std::nth_element(lum.begin(), lum.begin() + index, lum.end(), [&](double a, double b) { return key(a) < key(b); });
+  return 1e-3 * lum[index];
+}
+
+double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adaptive_config* cfg) {
+  if (cfg && cfg->has_minimum_luminance) return cfg->minimum_luminance;
+  if (!lum || n == 0) return 0.0;
+  std::vector<double> v(lum, lum + n);
+  return relative_min_luminance(v);
+}
+
 int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
                        uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza,
                        double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats) {
@@ -750,23 +772,12 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
   if (supersampled) {
     // resolve_minimum_luminance (raytracer.rs:118-129): exact 99th percentile in
     // f64::total_cmp order, selected on the host from the device 1-spp buffer.
-    double min_lum = 0.0;
-    std::vector<double> x64(4 * n);
-    HIP_TRY(hipMemcpy(x64.data(), b_x64.p, n * 32, hipMemcpyDeviceToHost));
-    if (cfg->has_minimum_luminance) {
-      min_lum = cfg->minimum_luminance;
-    } else {
-      std::vector<double> lum(n);
+    double min_lum = cfg->minimum_luminance;
+    if (!cfg->has_minimum_luminance) {
+      std::vector<double> x64(4 * n), lum(n);
+      HIP_TRY(hipMemcpy(x64.data(), b_x64.p, n * 32, hipMemcpyDeviceToHost));
       for (uint64_t i = 0; i < n; ++i) lum[i] = x64[4 * i + 1];
-      uint64_t index = (uint64_t)((double)(n - 1) * 0.99);
-      auto key = [](double v) {
-        int64_t b;
-        std::memcpy(&b, &v, 8);
-        return b ^ (int64_t)((uint64_t)(b >> 63) >> 1);
-      };
-      std::nth_element(lum.begin(), lum.begin() + index, lum.end(),
-                       [&](double a, double b) { return key(a) < key(b); });
-      min_lum = 1e-3 * lum[index];
+      min_lum = relative_min_luminance(lum);
     }
     grt::AdaptiveParams ap;
     ap.w = w;
@@ -907,6 +918,86 @@ int grt_render_shard_async(grt_scene* s, int device, void* stream, const grt_row
   HIP_TRY(hipSetDevice(device));
   grt::Outputs o{d_xyza, d_class, d_status, d_xyza64, d_steps, d_stop};
   return enqueue_trace(s, *dc, wl, o, (unsigned long long*)d_stats, (hipStream_t)stream);
+}
+
+int grt_supersample_shard(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
+                          const grt_adaptive_config* cfg, double min_lum, const double* d_frame_ya,
+                          const uint8_t* d_frame_class, const double* sampling_mask_xyza, double* d_xyza64,
+                          uint64_t* n_supersampled, uint64_t* d_stats) {
+  if (!s || !cfg || !d_frame_ya || !d_frame_class || !d_xyza64 || !d_stats) return fail(-EINVAL, "null argument");
+  if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
+  int rc = check_shard(sh);
+  if (rc) return rc;
+  if (n_supersampled) *n_supersampled = 0;
+  const uint32_t frame_rows = (uint32_t)s->desc.camera.rows, w = (uint32_t)s->desc.camera.cols;
+  const uint32_t local_rows = grt_shard_row_count(frame_rows, sh);
+  const uint64_t n_local = (uint64_t)local_rows * w;
+  if (n_local == 0) return 0;
+  DeviceCopy* dc;
+  if ((rc = ensure_device(s, device, &dc))) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t st = (hipStream_t)stream;
+  // collect_pixels_to_supersample (raytracer.rs:386-458) over this shard's pixels, with
+  // the whole frame's 1-spp buffer as the neighbourhood
+  grt::AdaptiveParams ap;
+  ap.w = w;
+  ap.h = frame_rows;
+  ap.exclude_background_contrast = cfg->exclude_background_contrast;
+  ap.min_lum = min_lum;
+  ap.luminance_contrast_threshold = cfg->luminance_contrast_threshold;
+  ap.opacity_contrast_threshold = cfg->opacity_contrast_threshold;
+  DevBuf b_flags;
+  if ((rc = b_flags.alloc(n_local))) return rc;
+  HIP_TRY(grt::launch_select_shard(d_frame_ya, d_frame_class, ap, sh->band_rows, sh->shard, sh->n_shards, local_rows,
+                                   (uint8_t*)b_flags.p, st));
+  std::vector<uint8_t> flags(n_local);
+  HIP_TRY(hipMemcpyAsync(flags.data(), b_flags.p, n_local, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  // selected pixels in frame order (shard rows increase with local rows): frame index for
+  // the jitter hash and the camera ray, local index for the output
+  std::vector<uint32_t> sel_frame, sel_local;
+  for (uint64_t i = 0; i < n_local; ++i)
+    if (flags[i]) {
+      uint64_t row = grt::shard_frame_row(sh->band_rows, sh->shard, sh->n_shards, (uint32_t)(i / w));
+      sel_frame.push_back((uint32_t)(row * w + i % w));
+      sel_local.push_back((uint32_t)i);
+    }
+  const uint64_t n_sel = sel_local.size();
+  if (n_supersampled) *n_supersampled = n_sel;
+  if (n_sel == 0) return 0;
+  DevBuf b_sel_frame, b_sel_local;
+  if ((rc = b_sel_frame.alloc(n_sel * 4)) || (rc = b_sel_local.alloc(n_sel * 4))) return rc;
+  HIP_TRY(hipMemcpyAsync(b_sel_local.p, sel_local.data(), n_sel * 4, hipMemcpyHostToDevice, st));
+  if (sampling_mask_xyza) {  // raytracer.rs:285-295: paint instead of supersampling
+    HIP_TRY(grt::launch_paint((const uint32_t*)b_sel_local.p, n_sel, sampling_mask_xyza, d_xyza64, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
+  HIP_TRY(hipMemcpyAsync(b_sel_frame.p, sel_frame.data(), n_sel * 4, hipMemcpyHostToDevice, st));
+  // supersample (raytracer.rs:320-384): samples_per_axis^2 jittered rays per pixel
+  const uint32_t spa = cfg->samples_per_axis;
+  const uint64_t ns = n_sel * spa * spa;
+  DevBuf b_pix, b_dx, b_dy, s_xyza, s_cls, s_status, s_x64;
+  if ((rc = b_pix.alloc(ns * 4)) || (rc = b_dx.alloc(ns * 8)) || (rc = b_dy.alloc(ns * 8)) ||
+      (rc = s_xyza.alloc(ns * 16)) || (rc = s_cls.alloc(ns)) || (rc = s_status.alloc(ns)) || (rc = s_x64.alloc(ns * 32)))
+    return rc;
+  HIP_TRY(grt::launch_make_offsets((const uint32_t*)b_sel_frame.p, n_sel, spa, 0, 0, w, (uint32_t*)b_pix.p,
+                                   (double*)b_dx.p, (double*)b_dy.p, st));
+  grt::WorkList wo;
+  std::memset(&wo, 0, sizeof(wo));
+  wo.rows = frame_rows;
+  wo.cols = w;
+  wo.n_items = ns;
+  wo.pixel_index = (const uint32_t*)b_pix.p;
+  wo.dx = (const double*)b_dx.p;
+  wo.dy = (const double*)b_dy.p;
+  grt::Outputs so{(float*)s_xyza.p, (uint8_t*)s_cls.p, (uint8_t*)s_status.p, (double*)s_x64.p, nullptr, nullptr};
+  if ((rc = enqueue_trace(s, *dc, wo, so, (unsigned long long*)d_stats, st))) return rc;
+  HIP_TRY(grt::launch_average((const uint32_t*)b_sel_local.p, n_sel, spa, (const double*)s_x64.p,
+                              (const uint8_t*)s_status.p, d_xyza64, st));
+  HIP_TRY(hipStreamSynchronize(st));  // the scratch buffers are freed on return
+  return 0;
 }
 
 }  // extern "C"

@@ -49,6 +49,9 @@ struct AdaptiveParams {
 };
 hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const AdaptiveParams& p,
                          uint8_t* d_flags, hipStream_t stream);
+hipError_t launch_select_shard(const double* d_ya, const uint8_t* d_cls, const AdaptiveParams& p, uint32_t band_rows,
+                               uint32_t shard, uint32_t n_shards, uint32_t local_rows, uint8_t* d_flags,
+                               hipStream_t stream);
 hipError_t launch_make_offsets(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, uint32_t row0,
                                uint32_t col0, uint32_t w, uint32_t* d_pix, double* d_dx, double* d_dy,
                                hipStream_t stream);

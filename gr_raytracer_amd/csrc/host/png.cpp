@@ -6,6 +6,7 @@
 // Radiance .hdr (RGBE) for the `.hdr` output path.
 #include <zlib.h>
 
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -220,3 +221,34 @@ bool hdr_encode_rgb(const std::string& path, const float* rgb, uint32_t w, uint3
 }
 
 }  // namespace grt_host
+
+// ---- C ABI: the image files Raytracer::render_section writes (raytracer.rs:460-497) ----
+extern "C" int grt_write_png_rgb(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height) {
+  if (!path || (!rgb && width && height)) {
+    grt_host::set_error("null argument");
+    return -EINVAL;
+  }
+  std::string err;
+  if (!grt_host::png_encode_rgb(path, rgb, width, height, err)) {
+    grt_host::set_error(err);
+    return -EIO;
+  }
+  return 0;
+}
+
+extern "C" int grt_write_hdr_xyz(const char* path, const double* xyza, uint32_t width, uint32_t height) {
+  if (!path || (!xyza && width && height)) {
+    grt_host::set_error("null argument");
+    return -EINVAL;
+  }
+  // XYZ stored as the RGB channels of an f32 Radiance image (raytracer.rs:468-480)
+  std::vector<float> rgb((size_t)width * height * 3);
+  for (size_t i = 0; i < (size_t)width * height; ++i)
+    for (int k = 0; k < 3; ++k) rgb[3 * i + k] = (float)xyza[4 * i + k];
+  std::string err;
+  if (!grt_host::hdr_encode_rgb(path, rgb.data(), width, height, err)) {
+    grt_host::set_error(err);
+    return -EIO;
+  }
+  return 0;
+}

@@ -56,36 +56,78 @@ def unpack_records(rec):
     return xyza, rec[:, 16].contiguous(), rec[:, 17].contiguous()
 
 
+def _padded_send(records, frame_rows: int, cols: int, band_rows: int, rank: int, world: int, device):
+    """This rank's records, zero-padded to the largest shard (equal-sized collective
+    buffers), on the collective's device."""
+    import torch
+
+    max_rows = shard_row_count(frame_rows, band_rows, 0, world)  # shard 0 owns the most bands
+    n_local = shard_row_count(frame_rows, band_rows, rank, world) * cols
+    width = records.shape[1]
+    assert records.shape == (n_local, width), (records.shape, n_local)
+    if n_local == max_rows * cols and records.device == device:
+        return records.contiguous()
+    send = torch.zeros((max_rows * cols, width), dtype=torch.uint8, device=device)
+    send[:n_local] = records
+    return send
+
+
+def _assemble(bufs, frame_rows: int, cols: int, band_rows: int, world: int, device):
+    """De-interleave every shard's local rows into frame order."""
+    import torch
+
+    width = bufs[0].shape[1]
+    frame = torch.empty((frame_rows, cols, width), dtype=torch.uint8, device=device)
+    for s in range(world):
+        rows = shard_frame_rows(frame_rows, band_rows, s, world)
+        if rows.size == 0:
+            continue
+        idx = torch.as_tensor(rows, device=device)
+        frame.index_copy_(0, idx, bufs[s][: rows.size * cols].view(rows.size, cols, width))
+    return frame.view(frame_rows * cols, width)
+
+
+def _collective_device(records, group=None):
+    """gloo moves host tensors only: device records are staged through the host when the
+    group's backend is gloo (multi-process tests on one GPU); RCCL works in place."""
+    import torch
+    import torch.distributed as dist
+
+    if records.device.type != "cpu" and dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return records.device
+
+
 def gather_frame(records, frame_rows: int, cols: int, band_rows: int, rank: int, world: int, dst: int = 0,
                  group=None):
     """Gather every rank's local pixel records to `dst` and put them in frame order.
 
     records: (local_rows * cols, B) uint8 on this rank's device (CPU for gloo), B = 18
     for pixel records, 3 for tone-mapped sRGB.
-    Returns the (frame_rows * cols, B) frame on `dst`, None elsewhere."""
+    Returns the (frame_rows * cols, B) frame on `dst` (on the records' device), None elsewhere."""
     import torch
     import torch.distributed as dist
 
-    max_rows = shard_row_count(frame_rows, band_rows, 0, world)  # shard 0 owns the most bands
-    n_local = shard_row_count(frame_rows, band_rows, rank, world) * cols
-    width = records.shape[1]
-    assert records.shape == (n_local, width), (records.shape, n_local)
-    send = records
-    if n_local != max_rows * cols:  # equal-sized buffers for the collective
-        send = torch.zeros((max_rows * cols, width), dtype=torch.uint8, device=records.device)
-        send[:n_local] = records
+    cdev = _collective_device(records, group)
+    send = _padded_send(records, frame_rows, cols, band_rows, rank, world, cdev)
     bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
     dist.gather(send, gather_list=bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    frame = torch.empty((frame_rows, cols, width), dtype=torch.uint8, device=records.device)
-    for s in range(world):
-        rows = shard_frame_rows(frame_rows, band_rows, s, world)
-        if rows.size == 0:
-            continue
-        idx = torch.as_tensor(rows, device=records.device)
-        frame.index_copy_(0, idx, bufs[s][: rows.size * cols].view(rows.size, cols, width))
-    return frame.view(frame_rows * cols, width)
+    return _assemble(bufs, frame_rows, cols, band_rows, world, cdev).to(records.device)
+
+
+def allgather_frame(records, frame_rows: int, cols: int, band_rows: int, rank: int, world: int, group=None):
+    """gather_frame for every rank: the (frame_rows * cols, B) frame in frame order on
+    all ranks (the adaptive pass's 1-spp neighbourhood)."""
+    import torch
+    import torch.distributed as dist
+
+    cdev = _collective_device(records, group)
+    send = _padded_send(records, frame_rows, cols, band_rows, rank, world, cdev)
+    bufs = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(bufs, send, group=group)
+    return _assemble(bufs, frame_rows, cols, band_rows, world, cdev).to(records.device)
 
 
 def reduce_channel_maxima(max3, group=None):
@@ -94,6 +136,11 @@ def reduce_channel_maxima(max3, group=None):
     MAX, in place.  This is the output stage's one real exchange step."""
     import torch.distributed as dist
 
+    if _collective_device(max3, group) != max3.device:
+        host = max3.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.MAX, group=group)
+        max3.copy_(host)
+        return max3
     dist.all_reduce(max3, op=dist.ReduceOp.MAX, group=group)
     return max3
 
@@ -170,3 +217,121 @@ def render_frame_srgb(scene, rank: int, world: int, tone_mapping: int = 0, expos
         L.check(lib.grt_tonemap_async(device, stream.cuda_stream, xyza64.data_ptr(), n_local, tone_mapping,
                                       exposure, max3.data_ptr(), rgb.data_ptr()), "grt_tonemap_async")
         return gather_frame(rgb, rows, cols, band_rows, rank, world, dst, group)
+
+
+def pack_luminance_records(xyza64, cls):
+    """(n,4) f64 XYZA + (n,) u8 class -> (n, 17) u8: Y and alpha (f64) and the class, what
+    the selection stencil and the luminance floor read (should_supersample_pair,
+    raytracer.rs:91-108; resolve_minimum_luminance, :118-129)."""
+    import torch
+
+    n = xyza64.shape[0]
+    ya = torch.stack([xyza64[:, 1], xyza64[:, 3]], dim=1).contiguous()
+    return torch.cat([ya.view(torch.uint8).view(n, 16), cls.view(n, 1)], dim=1)
+
+
+def unpack_luminance_records(rec):
+    import torch
+
+    n = rec.shape[0]
+    return rec[:, :16].contiguous().view(torch.float64).view(n, 2), rec[:, 16].contiguous()
+
+
+def pack_section_records(xyza64, cls, status):
+    """(n,4) f64 XYZA + class + status -> (n, 34) u8 (the supersampled frame's records)."""
+    import torch
+
+    n = xyza64.shape[0]
+    return torch.cat([xyza64.contiguous().view(torch.uint8).view(n, 32), cls.view(n, 1), status.view(n, 1)], dim=1)
+
+
+def unpack_section_records(rec):
+    import torch
+
+    n = rec.shape[0]
+    return rec[:, :32].contiguous().view(torch.float64).view(n, 4), rec[:, 32].contiguous(), rec[:, 33].contiguous()
+
+
+def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int = 16, device: int = 0,
+                          stream=None, dst: int = 0, group=None, stats=None, sampling_mask_xyza=None,
+                          tone_mapping=None, exposure: float = 1.0):
+    """render_section_to_cie_buffer (raytracer.rs:177-318) for a whole frame across
+    `world` GPUs, with the reference's adaptive supersampling:
+
+    1. each rank traces its row bands at 1 spp (f64 XYZA kept on the device);
+    2. ONE allgather of every pixel's (Y, alpha, class), 17 B per pixel: the selection
+       stencil reads 8 neighbours, which may sit in another rank's bands, and the
+       luminance floor is the 99th percentile of the whole frame;
+    3. every rank computes the same exact floor (grt_adaptive_min_luminance);
+    4. each rank selects and supersamples its own pixels (grt_supersample_shard);
+    5. ONE gather to `dst`: f64 XYZA + class + status (34 B per pixel), or, with
+       `tone_mapping` (0 Reinhard, 1 GlobalLinear), the per-rank tone-mapped sRGB8 rows
+       (3 B per pixel; GlobalLinear allreduces the channel maxima first).
+
+    cfg: grt_adaptive_config (default: the scene's own).  `enabled` false and no mask:
+    plain 1-spp frame (render_section_to_cie_buffer_raw).  Returns on dst
+    (xyza64 (n,4) f64, class u8, status u8, n_supersampled over all ranks) or, with
+    tone_mapping, (rgb (n,3) u8, n_supersampled); None elsewhere."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib as L
+
+    if cfg is None:
+        cfg = scene.adaptive
+    dev = torch.device("cuda", device)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    rows, cols = scene.rows, scene.cols
+    n_local = shard_row_count(rows, band_rows, rank, world) * cols
+    xyza = torch.empty((n_local, 4), dtype=torch.float32, device=dev)
+    xyza64 = torch.empty((n_local, 4), dtype=torch.float64, device=dev)
+    cls = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    status = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    if stats is None:
+        stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    sh = L.RowShard(band_rows, rank, world)
+    lib = L.lib()
+    L.check(lib.grt_render_shard_async(scene._s, device, stream.cuda_stream, C.byref(sh), xyza.data_ptr(),
+                                       cls.data_ptr(), status.data_ptr(), xyza64.data_ptr(), None, None,
+                                       stats.data_ptr()), "grt_render_shard_async")
+    n_sel = torch.zeros(1, dtype=torch.int64)
+    with torch.cuda.stream(stream):
+        if cfg.enabled or sampling_mask_xyza is not None:
+            frame = allgather_frame(pack_luminance_records(xyza64, cls), rows, cols, band_rows, rank, world, group)
+            frame_ya, frame_cls = unpack_luminance_records(frame)
+            if cfg.has_minimum_luminance:
+                min_lum = cfg.minimum_luminance
+            else:
+                lum = np.ascontiguousarray(frame_ya[:, 0].cpu().numpy())
+                min_lum = lib.grt_adaptive_min_luminance(L.dptr(lum), lum.shape[0], C.byref(cfg))
+            mask = None
+            if sampling_mask_xyza is not None:
+                mask = (C.c_double * 4)(*[float(v) for v in sampling_mask_xyza])
+            count = C.c_uint64(0)
+            L.check(lib.grt_supersample_shard(scene._s, device, stream.cuda_stream, C.byref(sh), C.byref(cfg),
+                                              min_lum, frame_ya.data_ptr(), frame_cls.data_ptr(), mask,
+                                              xyza64.data_ptr(), C.byref(count), stats.data_ptr()),
+                    "grt_supersample_shard")
+            total = torch.tensor([count.value], dtype=torch.int64, device=dev)
+            total = total.to(_collective_device(total, group))
+            dist.all_reduce(total, op=dist.ReduceOp.SUM, group=group)
+            n_sel[0] = int(total[0])
+        if tone_mapping is not None:
+            rgb = torch.empty((n_local, 3), dtype=torch.uint8, device=dev)
+            max3 = torch.zeros(3, dtype=torch.float64, device=dev)
+            if tone_mapping == 1:
+                L.check(lib.grt_linear_max_async(device, stream.cuda_stream, xyza64.data_ptr(), n_local, exposure,
+                                                 max3.data_ptr()), "grt_linear_max_async")
+                reduce_channel_maxima(max3, group)
+            L.check(lib.grt_tonemap_async(device, stream.cuda_stream, xyza64.data_ptr(), n_local, tone_mapping,
+                                          exposure, max3.data_ptr(), rgb.data_ptr()), "grt_tonemap_async")
+            out = gather_frame(rgb, rows, cols, band_rows, rank, world, dst, group)
+            return None if out is None else (out, int(n_sel[0]))
+        out = gather_frame(pack_section_records(xyza64, cls, status), rows, cols, band_rows, rank, world, dst, group)
+    if out is None:
+        return None
+    x64, c, st = unpack_section_records(out)
+    return x64, c, st, int(n_sel[0])

@@ -1,0 +1,157 @@
+"""Multi-GPU `render`: the reference's `render` subcommand with the frame split across
+the GPUs of a node (BASELINE config C4).
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        -m gr_raytracer_amd.render_dist --width=4096 --height=4096 --max-steps=1000000 \\
+        --camera-position=-10,0,-0.5 --theta=1.52 --psi=-1.57 --phi=0 \\
+        --config-file scene-definitions/kerr.toml render --filename kerr.png
+
+The flags are the reference's (cli.rs:5-113, the same set as the single-GPU `grt`
+binary); `--resource-root DIR` resolves texture paths and `--raw-out FILE` dumps the
+f64 XYZA frame, as in `grt`.  One process per GPU: rank r uses GPU LOCAL_RANK, traces
+the cyclic row bands b with b % world == r, and the frame is assembled on rank 0 with
+one RCCL gather (plus, for the stock TOMLs' adaptive supersampling, one allgather of
+the 1-spp luminance, opacity and class; gr_raytracer_amd.distributed).  The pixels are
+identical to a single-GPU `grt ... render` of the same scene.  Sections (--from-row ...)
+are single-GPU only (use `grt`).  Without torchrun it runs as a world of one.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+RENDER_FLAGS = ("--filename", "--from-row", "--from-col", "--to-row", "--to-col")
+
+
+def _csv(n: int, conv=float):
+    def parse(v: str):
+        parts = v.split(",")
+        if len(parts) != n:
+            raise argparse.ArgumentTypeError(f"expected {n} comma-separated values, got {v!r}")
+        return [conv(p) for p in parts]
+    return parse
+
+
+def parse_args(argv):
+    """cli.rs:5-113 for `render`: global options anywhere, then the subcommand."""
+    p = argparse.ArgumentParser(prog="render_dist", description=__doc__.splitlines()[0])
+    p.add_argument("--width", type=int, default=500)
+    p.add_argument("--height", type=int, default=500)
+    p.add_argument("--step-size", type=float, default=0.01)
+    p.add_argument("--max-steps", type=int, default=20000)
+    p.add_argument("--max-radius", type=float, default=15000.0)
+    p.add_argument("--epsilon", type=float, default=0.00001)
+    p.add_argument("--camera-position", type=_csv(3), default=[18.0, 0.0, 0.8])
+    p.add_argument("--phi", type=float, default=0.0)
+    p.add_argument("--theta", type=float, default=0.0)
+    p.add_argument("--psi", type=float, default=0.0)
+    p.add_argument("--tone-mapping", choices=["reinhard", "global-linear"], default="reinhard")
+    p.add_argument("--show-sampling-mask", action="store_true")
+    p.add_argument("--sampling-mask-color", type=_csv(3, int), default=[255, 0, 255])
+    p.add_argument("-c", "--config-file", required=True)
+    p.add_argument("--resource-root", default=None)
+    p.add_argument("--raw-out", default=None)
+    p.add_argument("--band-rows", type=int, default=16, help="rows per cyclic band (not in the reference)")
+    p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
+    p.add_argument("action", choices=["render"])
+    p.add_argument("--filename", default="render.png")
+    for f in RENDER_FLAGS[1:]:
+        p.add_argument(f, type=int, default=None)
+    a = p.parse_args(argv)
+    if any(getattr(a, f[2:].replace("-", "_")) is not None for f in RENDER_FLAGS[1:]):
+        p.error("sections (--from-row/--from-col/--to-row/--to-col) are single-GPU only: use grt")
+    for k in a.sampling_mask_color:
+        if not 0 <= k <= 255:
+            p.error("invalid RGB color; expected R,G,B")
+    return a
+
+
+def main(argv=None) -> int:
+    a = parse_args(sys.argv[1:] if argv is None else argv)
+    t_start = time.perf_counter()
+    import ctypes as C
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib as L
+    from .distributed import render_frame_adaptive
+    from .scene import GlobalOpts, load_scene
+
+    if "WORLD_SIZE" not in os.environ:  # plain `python -m`: a world of one
+        os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                           "MASTER_PORT": os.environ.get("MASTER_PORT", "29531")})
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = torch.cuda.device_count()
+    if n_dev == 0:
+        raise L.GrtError("no GPU visible: render_dist runs the HIP kernels only (there is no CPU path)")
+    device = local_rank % n_dev
+    torch.cuda.set_device(device)
+    backend = a.backend or "nccl"
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+    else:
+        dist.init_process_group(backend)
+    try:
+        opts = GlobalOpts(width=a.width, height=a.height, step_size=a.step_size, max_steps=a.max_steps,
+                          max_radius=a.max_radius, epsilon=a.epsilon, camera_position=a.camera_position, phi=a.phi,
+                          theta=a.theta, psi=a.psi, tone_mapping=a.tone_mapping,
+                          show_sampling_mask=a.show_sampling_mask, sampling_mask_color=a.sampling_mask_color)
+        scene = load_scene(a.config_file, opts, a.resource_root)
+        mask = None
+        if a.show_sampling_mask:
+            mask = np.zeros(4)
+            r, g, b = a.sampling_mask_color
+            L.lib().grt_srgb_to_xyza(r, g, b, 255, L.dptr(mask))
+        tone = {"reinhard": 0, "global-linear": 1}[a.tone_mapping]
+        want_f64 = a.filename.endswith(".hdr") or a.raw_out is not None
+        stats = torch.zeros(4, dtype=torch.int64, device=torch.device("cuda", device))
+        dist.barrier()
+        t0 = time.perf_counter()
+        out = render_frame_adaptive(scene, rank, world, band_rows=a.band_rows, device=device, stats=stats,
+                                    sampling_mask_xyza=mask, tone_mapping=None if want_f64 else tone)
+        torch.cuda.synchronize()
+        t_render = time.perf_counter() - t0
+        if dist.get_backend() == "gloo":
+            host = stats.cpu()
+            dist.all_reduce(host)
+            totals = host
+        else:
+            dist.all_reduce(stats)
+            totals = stats.cpu()
+        if rank != 0:
+            return 0
+        w, h = scene.cols, scene.rows
+        if want_f64:
+            xyza64, _cls, _status, n_sel = out
+            x = np.ascontiguousarray(xyza64.cpu().numpy())
+            if a.raw_out is not None:
+                x.tofile(a.raw_out)
+            if a.filename.endswith(".hdr"):
+                L.check(L.lib().grt_write_hdr_xyz(a.filename.encode(), L.dptr(x), w, h), "grt_write_hdr_xyz")
+            else:
+                rgb = np.zeros((w * h, 3), np.uint8)
+                L.check(L.lib().grt_xyz_to_srgb8_device(device, L.dptr(x), w * h, tone, 1.0,
+                                                        L.ptr(rgb, C.c_uint8)), "grt_xyz_to_srgb8_device")
+                L.check(L.lib().grt_write_png_rgb(a.filename.encode(), L.ptr(rgb, C.c_uint8), w, h),
+                        "grt_write_png_rgb")
+        else:
+            rgb_t, n_sel = out
+            rgb = np.ascontiguousarray(rgb_t.cpu().numpy())
+            L.check(L.lib().grt_write_png_rgb(a.filename.encode(), L.ptr(rgb, C.c_uint8), w, h), "grt_write_png_rgb")
+        steps = int(totals[0])
+        print(f"[render_dist] {world} GPU(s): {int(totals[2])} rays, {steps} accepted steps, {int(totals[1])} attempts, "
+              f"{n_sel} supersampled pixels, frame {t_render:.3f} s ({steps / t_render:.3e} steps/s)",
+              file=sys.stderr)
+        print(f"saved image to {a.filename}\nElapsed time: {time.perf_counter() - t_start:.3f} s", file=sys.stderr)
+        return 0
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

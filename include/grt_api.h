@@ -389,6 +389,40 @@ int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt
                            float* d_xyza, uint8_t* d_class, uint8_t* d_status, double* d_xyza64,
                            uint32_t* d_steps, uint8_t* d_stop, uint64_t* d_stats);
 
+/* ---- adaptive supersampling of a frame split across GPUs -------
+ * render_section_to_cie_buffer_supersampled (raytracer.rs:257-318) with the frame's
+ * rows spread over processes.  Per rank:
+ *   1. grt_render_shard_async(..., d_xyza64, ...): the 1-spp pass of its row bands;
+ *   2. allgather of every pixel's (Y, alpha) and class, frame order (17 B per pixel:
+ *      the selection stencil reads its 8 neighbours, which may belong to other ranks,
+ *      and the luminance floor is a percentile over the whole frame);
+ *   3. grt_adaptive_min_luminance over the frame's Y: identical on every rank;
+ *   4. grt_supersample_shard: selection of the shard's pixels, samples_per_axis^2
+ *      jittered rays per selected pixel, ordered average into the shard's f64 XYZA.
+ * The result is identical to grt_render_section over the whole frame. */
+
+/* resolve_minimum_luminance (raytracer.rs:118-129): cfg->minimum_luminance when set,
+ * else 1e-3 x the ((n-1) * 0.99)-th luminance in f64::total_cmp order (0 when n = 0). */
+double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adaptive_config* cfg);
+
+/* collect_pixels_to_supersample (raytracer.rs:386-458) over the local pixels of shard
+ * `sh` + supersample (:320-384), on `device`, enqueued on `stream` and synchronised
+ * before returning (the selection count sizes the second trace).
+ * d_frame_ya: (Y, alpha) per frame pixel, 2 f64, frame order; d_frame_class: RayClass
+ * per frame pixel; d_xyza64: the shard's 1-spp f64 XYZA (local rows, grt_render_shard
+ * order), overwritten in place for the selected pixels; sampling_mask_xyza (host,
+ * 4 f64, nullable): paint the selected pixels instead (--show-sampling-mask,
+ * raytracer.rs:285-295).  d_stats: 4 uint64 device counters, accumulated. */
+int grt_supersample_shard(grt_scene* scene, int device, void* stream, const grt_row_shard* sh,
+                          const grt_adaptive_config* cfg, double min_lum, const double* d_frame_ya,
+                          const uint8_t* d_frame_class, const double* sampling_mask_xyza,
+                          double* d_xyza64, uint64_t* n_supersampled, uint64_t* d_stats);
+
+/* The image files of Raytracer::render_section (raytracer.rs:460-497): an 8-bit RGB
+ * PNG, and the Radiance .hdr that stores XYZ as its RGB channels (f32, RGBE). */
+int grt_write_png_rgb(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+int grt_write_hdr_xyz(const char* path, const double* xyza, uint32_t width, uint32_t height);
+
 /* ---- whole trajectories (render-ray / render-ray-at) ------ */
 /* Integrator::integrate keeping every Step (integrator.rs:78-174), as
  * Raytracer::integrate_ray_at_point (raytracer.rs:499-507, `render-ray`) and

@@ -1,0 +1,235 @@
+"""Adaptive supersampling of a frame split across GPUs.
+
+render_section_to_cie_buffer_supersampled (raytracer.rs:257-318) needs, for each pixel,
+its 8 neighbours' 1-spp colour and class, and a luminance floor that is a percentile
+of the WHOLE frame.  With cyclic row bands those neighbours belong to other ranks, so
+the ranks allgather (Y, alpha, class) once, then select and supersample their own
+pixels (grt_supersample_shard).  The bar: the assembled frame equals a single-process
+grt_render_section of the same frame bit for bit (colour, class, selection count).
+
+CPU: the exact percentile (grt_adaptive_min_luminance) against a total_cmp sort, the
+allgather assembly over gloo (world 2 and 3), record packing, the CLI flags.
+GPU: in-process shards against grt_render_section, and the multi-process `render_dist`
+CLI (2 ranks on one GPU over gloo) against the single-GPU `grt` binary.
+"""
+import ctypes as C
+import os
+import socket
+import struct
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import RESOURCES, ROOT, SCENES, c2_opts, host_scene
+
+
+def _total_cmp_key(v: float) -> int:
+    b = struct.unpack("<q", struct.pack("<d", v))[0]
+    return b ^ ((b >> 63) & 0x7FFFFFFFFFFFFFFF)
+
+
+def _ref_floor(lum):
+    """resolve_minimum_luminance (raytracer.rs:118-129) by a full total_cmp sort."""
+    if len(lum) == 0:
+        return 0.0
+    s = sorted(lum.tolist(), key=_total_cmp_key)
+    return 1e-3 * s[int((len(lum) - 1) * 0.99)]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 99, 100, 101, 1000, 4097])
+def test_min_luminance_is_the_total_cmp_percentile(grt, n):
+    from gr_raytracer_amd import _lib as L
+
+    rng = np.random.default_rng(n)
+    lum = rng.exponential(size=n) * rng.choice([1e-9, 1.0, 1e3], size=n)
+    if n > 10:  # signed zeros, NaNs of both signs, infinities: total_cmp places them all
+        lum[:6] = [0.0, -0.0, np.inf, -np.inf, np.nan, -np.nan]
+        rng.shuffle(lum)
+    cfg = L.AdaptiveConfig()
+    L.lib().grt_default_adaptive_config(C.byref(cfg))
+    cfg.has_minimum_luminance = 0
+    lum = np.ascontiguousarray(lum)
+    got = L.lib().grt_adaptive_min_luminance(L.dptr(lum) if n else None, n, C.byref(cfg))
+    want = _ref_floor(lum)
+    assert struct.pack("<d", got) == struct.pack("<d", want) or (np.isnan(got) and np.isnan(want))
+    cfg.has_minimum_luminance = 1
+    cfg.minimum_luminance = 0.25
+    assert L.lib().grt_adaptive_min_luminance(L.dptr(lum) if n else None, n, C.byref(cfg)) == 0.25
+
+
+def test_luminance_and_section_records_round_trip():
+    import torch
+
+    from gr_raytracer_amd.distributed import (pack_luminance_records, pack_section_records, unpack_luminance_records,
+                                              unpack_section_records)
+
+    rng = np.random.default_rng(3)
+    x = torch.from_numpy(rng.normal(size=(37, 4)))
+    c = torch.from_numpy(rng.integers(0, 3, 37).astype(np.uint8))
+    s = torch.from_numpy(rng.integers(0, 9, 37).astype(np.uint8))
+    ya, cc = unpack_luminance_records(pack_luminance_records(x, c))
+    assert torch.equal(ya[:, 0], x[:, 1]) and torch.equal(ya[:, 1], x[:, 3]) and torch.equal(cc, c)
+    x2, c2, s2 = unpack_section_records(pack_section_records(x, c, s))
+    assert torch.equal(x2, x) and torch.equal(c2, c) and torch.equal(s2, s)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+ROWS, COLS = 37, 11
+
+
+def _allgather_worker(rank, world, port, band_rows, out_dir):
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+
+    from gr_raytracer_amd.distributed import allgather_frame, shard_frame_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows = shard_frame_rows(ROWS, band_rows, rank, world)
+        # record of frame pixel (r, c): 5 bytes spelling its row and column
+        rec = np.zeros((len(rows) * COLS, 5), np.uint8)
+        for k, r in enumerate(rows):
+            for c in range(COLS):
+                rec[k * COLS + c] = [r, c, 7, rank, 255]
+        frame = allgather_frame(torch.from_numpy(rec), ROWS, COLS, band_rows, rank, world)
+        np.save(os.path.join(out_dir, f"frame{rank}.npy"), frame.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,band_rows", [(2, 8), (3, 4)])
+def test_gloo_allgather_puts_every_pixel_in_frame_order(world, band_rows):
+    import torch.multiprocessing as mp
+
+    from gr_raytracer_amd.distributed import shard_frame_rows
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_allgather_worker, args=(world, _free_port(), band_rows, d), nprocs=world, join=True)
+        owner = np.zeros(ROWS, np.uint8)
+        for s in range(world):
+            owner[shard_frame_rows(ROWS, band_rows, s, world)] = s
+        want = np.array([[r, c, 7, owner[r], 255] for r in range(ROWS) for c in range(COLS)], np.uint8)
+        for rank in range(world):
+            assert np.array_equal(np.load(os.path.join(d, f"frame{rank}.npy")), want)
+
+
+def test_render_dist_flags():
+    from gr_raytracer_amd.render_dist import parse_args
+
+    a = parse_args(["--width=4096", "--height", "4096", "--max-steps=1000000", "--camera-position=-10,0,-0.5",
+                    "--theta=1.52", "--psi=-1.57", "--config-file", "kerr.toml", "render", "--filename", "k.png"])
+    assert (a.width, a.height, a.max_steps, a.theta, a.psi) == (4096, 4096, 1000000, 1.52, -1.57)
+    assert a.camera_position == [-10.0, 0.0, -0.5] and a.filename == "k.png" and a.tone_mapping == "reinhard"
+    with pytest.raises(SystemExit):
+        parse_args(["--config-file", "x.toml", "render", "--from-row", "3"])
+    with pytest.raises(SystemExit):
+        parse_args(["--config-file", "x.toml", "--sampling-mask-color=1,2,300", "render"])
+
+
+# ------------------------------------------------------------------------ GPU --
+def _frame_adaptive(grt, width=72, height=64, spa=4):
+    hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=width, height=height))
+    ad = hs.adaptive
+    ad.enabled = 1
+    ad.samples_per_axis = spa
+    return hs, ad
+
+
+def _supersample_in_process(grt, sc, ad, n_shards, band_rows, mask=None):
+    """Every rank's steps of render_frame_adaptive, one after another in this process,
+    with the allgather done by array assembly."""
+    import torch
+
+    from gr_raytracer_amd import _lib as L
+    from gr_raytracer_amd.distributed import shard_frame_rows
+
+    rows, cols = sc.rows, sc.cols
+    parts = [sc.render_shard(band_rows, s, n_shards) for s in range(n_shards)]
+    frame_x = np.zeros((rows, cols, 4))
+    frame_c = np.zeros((rows, cols), np.uint8)
+    for s, p in enumerate(parts):
+        r = shard_frame_rows(rows, band_rows, s, n_shards)
+        frame_x[r] = p.xyza64.reshape(len(r), cols, 4)
+        frame_c[r] = p.ray_class.reshape(len(r), cols)
+    lum = np.ascontiguousarray(frame_x[..., 1].ravel())
+    min_lum = L.lib().grt_adaptive_min_luminance(L.dptr(lum), lum.size, C.byref(ad))
+    dev = torch.device("cuda", 0)
+    d_ya = torch.from_numpy(np.ascontiguousarray(frame_x[..., [1, 3]].reshape(-1, 2))).to(dev)
+    d_cls = torch.from_numpy(frame_c.ravel()).to(dev)
+    out = np.zeros((rows, cols, 4))
+    n_sel = 0
+    for s, p in enumerate(parts):
+        d_x = torch.from_numpy(p.xyza64).to(dev)
+        stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        cnt = C.c_uint64(0)
+        sh = L.RowShard(band_rows, s, n_shards)
+        m = None if mask is None else (C.c_double * 4)(*mask)
+        L.check(L.lib().grt_supersample_shard(sc._s, 0, None, C.byref(sh), C.byref(ad), min_lum, d_ya.data_ptr(),
+                                              d_cls.data_ptr(), m, d_x.data_ptr(), C.byref(cnt), stats.data_ptr()),
+                "grt_supersample_shard")
+        n_sel += cnt.value
+        r = shard_frame_rows(rows, band_rows, s, n_shards)
+        out[r] = d_x.cpu().numpy().reshape(len(r), cols, 4)
+    return out.reshape(-1, 4), frame_c.ravel(), n_sel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_shards,band_rows", [(1, 16), (2, 8), (3, 16), (8, 8)])
+def test_shard_supersampling_equals_render_section(grt, gpu, n_shards, band_rows):
+    hs, ad = _frame_adaptive(grt)
+    sc = grt.Scene(hs.desc_ptr(), keepalive=hs, adaptive=ad)
+    want, want_cls, want_sel, _ = sc.render_section(adaptive=ad)
+    got, got_cls, got_sel = _supersample_in_process(grt, sc, ad, n_shards, band_rows)
+    assert want_sel > 0 and got_sel == want_sel
+    assert np.array_equal(got_cls, want_cls)
+    assert np.array_equal(got, want)  # bit for bit
+
+
+@pytest.mark.gpu
+def test_shard_sampling_mask_equals_render_section(grt, gpu):
+    hs, ad = _frame_adaptive(grt, spa=2)
+    sc = grt.Scene(hs.desc_ptr(), keepalive=hs, adaptive=ad)
+    mask = grt.srgb_to_xyza(255, 0, 255)
+    want, _, want_sel, _ = sc.render_section(adaptive=ad, sampling_mask_xyza=mask)
+    got, _, got_sel = _supersample_in_process(grt, sc, ad, 3, 8, mask=list(mask))
+    assert got_sel == want_sel > 0
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tone", ["reinhard", "global-linear"])
+def test_render_dist_two_ranks_equal_grt_cli(gpu, tone):
+    """`render_dist` with 2 ranks (gloo, both on GPU 0) writes the same PNG and the same
+    f64 frame as the single-GPU `grt` binary; the stock TOML supersamples adaptively."""
+    flags = ["--width=80", "--height=72", "--camera-position=-16.0,0.0,3.5", "--theta=-3.142",
+             "--max-steps=100000", f"--tone-mapping={tone}", "--config-file", str(SCENES / "schwarzschild.toml"),
+             "--resource-root", str(RESOURCES)]
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    with tempfile.TemporaryDirectory() as d:
+        ref_png, ref_raw = os.path.join(d, "ref.png"), os.path.join(d, "ref.raw")
+        subprocess.run([str(ROOT / "gr_raytracer_amd" / "lib" / "grt"), *flags, "--raw-out", ref_raw, "render",
+                        "--filename", ref_png], check=True, timeout=100, env=env)
+        png, raw, png2 = os.path.join(d, "d.png"), os.path.join(d, "d.raw"), os.path.join(d, "d2.png")
+        launch = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                  "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "gr_raytracer_amd.render_dist",
+                  "--backend=gloo", "--band-rows=8"]
+        subprocess.run([*launch, *flags, "--raw-out", raw, "render", "--filename", png], check=True, timeout=100,
+                       env=env, cwd=str(ROOT))
+        launch[5] = f"--master-port={_free_port()}"
+        subprocess.run([*launch, *flags, "render", "--filename", png2], check=True, timeout=100, env=env,
+                       cwd=str(ROOT))
+        assert np.array_equal(np.fromfile(raw), np.fromfile(ref_raw))
+        ref = open(ref_png, "rb").read()
+        assert open(png, "rb").read() == ref  # rank 0 tone-maps the gathered f64 frame
+        assert open(png2, "rb").read() == ref  # per-rank tone mapping, sRGB rows gathered
