@@ -63,7 +63,15 @@ def cpu_baseline(g, seconds_budget: float = 20.0) -> dict:
     t0 = time.time()
     r = O.render_pixels(hs.desc, 0, 0, 1500, 1500, threads=cores, row_list=rows)
     wall = time.time() - t0
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": r["accepted"] / r["wall_s"], "unit": "geodesic steps/s", "cores": cores, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(),
+            "full_frame_s_extrapolated": round(r["wall_s"] * 1500 / len(rows), 1),
             "sample": f"C2 frame rows 0 mod 64 ({len(rows)} rows x 1500 px = {len(rows) * 1500} rays, "
                       f"{r['accepted']} accepted steps in {r['wall_s']:.1f} s, OpenMP dynamic over pixels)",
             "wall_s": round(wall, 2)}
