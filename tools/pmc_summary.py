@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNEL = "grt::integrate_kernel<1, false>"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "grt::integrate_kernel<1, false>"
 
 
 def load(pass_dir):
@@ -41,7 +41,7 @@ def main():
     fetch_b = counters.get("FETCH_SIZE", 0.0) * 1024 * 2
     write_b = counters.get("WRITE_SIZE", 0.0) * 1024
     out = {
-        "kernel": f"{KERNEL} (Schwarzschild), one C2 frame (1500x1500, 2.25M rays)",
+        "kernel": f"{KERNEL}, one frame of tools/prof_target.py (1500x1500, 2.25M rays)",
         "source": "rocprofv3 --kernel-trace --pmc <one counter group per pass>, tools/run_pmc.sh",
         "counters": counters,
         "kernel_ms_per_pass": kernel_ms,

@@ -1,9 +1,10 @@
 #!/bin/bash
-# PMC passes (separate rocprofv3 runs, counters only with --kernel-trace) on one C2 frame.
+# PMC passes (separate rocprofv3 runs, counters only with --kernel-trace) on one frame.
+# Usage: tools/run_pmc.sh <tag> [c2|c3]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$1; mkdir -p $OUT
-T="python3 tools/prof_target.py c2"
+T="python3 tools/prof_target.py ${2:-c2}"
 P() { name=$1; shift; timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/$name -o run "$@" -- $T > $OUT/$name.log 2>&1; }
 P fetch --pmc FETCH_SIZE || exit 1
 P write --pmc WRITE_SIZE || exit 1
