@@ -2097,5 +2097,104 @@ void oracle_xyz_to_srgb8(const double* xyza, uint64_t n, int tone, double exposu
   }
 }
 
+
+// ---- geometry probes for the reference's unit tests (tests/test_reference_kats.py) ----
+// Each builds the scene's Geometry from the descriptor (geometry, radius, a,
+// horizon_epsilon) and calls one of the functions the path uses.
+int oracle_should_stop(const grt_scene_desc* d, const double* y, uint64_t i) {  // integrator.rs:203-268
+  SceneCtx S;
+  init_ctx(S, d);
+  return should_stop(*S.g, S.cfg, y, i);
+}
+int oracle_inside_horizon(const grt_scene_desc* d, const double* pos) {
+  SceneCtx S;
+  init_ctx(S, d);
+  return S.g->inside_horizon(S.g->make_point(pos)) ? 1 : 0;
+}
+// radial_coordinate of a native-chart point, or of a Cartesian one (cartesian != 0)
+double oracle_radial_coordinate(const grt_scene_desc* d, const double* pos, int cartesian) {
+  SceneCtx S;
+  init_ctx(S, d);
+  Point p = cartesian ? Point{CS::Cartesian, d->a, {pos[0], pos[1], pos[2], pos[3]}} : S.g->make_point(pos);
+  return S.g->radial_coordinate(p);
+}
+void oracle_to_cartesian(const grt_scene_desc* d, const double* pos, double* out) {  // point.rs:125-154
+  SceneCtx S;
+  init_ctx(S, d);
+  Point c = to_cartesian(S.g->make_point(pos));
+  for (int k = 0; k < 4; ++k) out[k] = c.v[k];
+}
+void oracle_stationary_velocity(const grt_scene_desc* d, const double* pos, double* out) {
+  SceneCtx S;
+  init_ctx(S, d);
+  FourVector u = S.g->stationary_velocity(S.g->make_point(pos));
+  for (int k = 0; k < 4; ++k) out[k] = u.v[k];
+}
+int oracle_circular_orbit_velocity(const grt_scene_desc* d, const double* pos, double* out) {
+  SceneCtx S;
+  init_ctx(S, d);
+  FourVector u{S.g->cs(), {0, 0, 0, 0}};
+  Err e = S.g->circular_orbit_velocity(S.g->make_point(pos), &u);
+  for (int k = 0; k < 4; ++k) out[k] = u.v[k];
+  return e;
+}
+// The solver of the ray (pos, mom): create_initial_state -> y0, apply(y_in or y0) ->
+// rhs, momentum_from_state(y_in or y0) -> p.  y_in may be NULL.
+void oracle_geodesic_rhs(const grt_scene_desc* d, const double* pos, const double* mom, const double* y_in,
+                         double* y0, double* rhs, double* p) {
+  SceneCtx S;
+  init_ctx(S, d);
+  Ray ray;
+  ray.row = ray.col = 0;
+  ray.position = S.g->make_point(pos);
+  ray.momentum = FourVector{S.g->cs(), {mom[0], mom[1], mom[2], mom[3]}};
+  std::unique_ptr<GeodesicSolver> sol = S.g->solver(ray);
+  sol->create_initial_state(ray, y0);
+  const double* y = y_in ? y_in : y0;
+  sol->apply(y, rhs);
+  FourVector f = sol->momentum_from_state(y);
+  for (int k = 0; k < 4; ++k) p[k] = f.v[k];
+}
+// kerr.rs:49-110 metric / metric_contravariant; kerr_bl.rs:253-272 metric_bl
+void oracle_ks_metric(double radius, double a, double x, double y, double z, int contravariant, double* g) {
+  Mat4 m = contravariant ? ks_metric_contravariant(radius, a, x, y, z) : ks_metric(radius, a, x, y, z);
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) g[4 * i + j] = m.m[i][j];
+}
+void oracle_bl_metric(double r_s, double a, double r, double theta, double* g) {
+  Mat4 m = metric_bl(r_s, a, r, theta);
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) g[4 * i + j] = m.m[i][j];
+}
+// RedshiftComputer::compute_redshift (redshift.rs:31-38, :62-73): static emitter at pos
+double oracle_redshift_static(const grt_scene_desc* d, const double* pos, const double* mom, double observer_energy) {
+  SceneCtx S;
+  init_ctx(S, d);
+  Point p = S.g->make_point(pos);
+  FourVector m{S.g->cs(), {mom[0], mom[1], mom[2], mom[3]}};
+  double emitter_energy = S.g->inner_product(p, S.g->stationary_velocity(p), m);
+  double sig0 = S.g->signature0();
+  return (sig0 * observer_energy) / (sig0 * emitter_energy);
+}
+// KerrBLSolver::geodesic (kerr_bl.rs:141-174) with explicit constants of motion
+void oracle_kerr_bl_rhs(double r_s, double a, double e, double l_z, double q, const double* y, double* out) {
+  KerrBLSolver sol;
+  sol.radius = r_s;
+  sol.a = a;
+  sol.e = e;
+  sol.l_z = l_z;
+  sol.q = q;
+  sol.apply(y, out);
+}
+// should_supersample_pair (raytracer.rs:91-108) on two (XYZA, class) samples
+int oracle_should_supersample_pair(const double* p, int pc, const double* q, int qc, const grt_adaptive_config* c,
+                                   double min_lum) {
+  Sample a, b;
+  a.color = XYZA{p[0], p[1], p[2], p[3]};
+  a.ray_class = pc;
+  b.color = XYZA{q[0], q[1], q[2], q[3]};
+  b.ray_class = qc;
+  return should_supersample_pair(a, b, *c, min_lum) ? 1 : 0;
+}
 }  // extern "C"
 

@@ -56,6 +56,20 @@ def lib():
         L.oracle_perlin_table.argtypes = [C.c_uint32, _u8p]
         L.oracle_perlin.restype = _d
         L.oracle_perlin.argtypes = [C.c_uint32, _d, _d, _d]
+        L.oracle_should_stop.argtypes = [vp, _pd, C.c_uint64]
+        L.oracle_inside_horizon.argtypes = [vp, _pd]
+        L.oracle_radial_coordinate.restype = _d
+        L.oracle_radial_coordinate.argtypes = [vp, _pd, C.c_int]
+        L.oracle_to_cartesian.argtypes = [vp, _pd, _pd]
+        L.oracle_stationary_velocity.argtypes = [vp, _pd, _pd]
+        L.oracle_circular_orbit_velocity.argtypes = [vp, _pd, _pd]
+        L.oracle_geodesic_rhs.argtypes = [vp, _pd, _pd, _pd, _pd, _pd, _pd]
+        L.oracle_ks_metric.argtypes = [_d, _d, _d, _d, _d, C.c_int, _pd]
+        L.oracle_bl_metric.argtypes = [_d, _d, _d, _d, _pd]
+        L.oracle_redshift_static.restype = _d
+        L.oracle_redshift_static.argtypes = [vp, _pd, _pd, _d]
+        L.oracle_kerr_bl_rhs.argtypes = [_d, _d, _d, _d, _d, _pd, _pd]
+        L.oracle_should_supersample_pair.argtypes = [_pd, C.c_int, _pd, C.c_int, vp, _d]
         L.oracle_vdisc_density.restype = _d
         L.oracle_vdisc_density.argtypes = [vp, C.c_int, _pd]
         L.oracle_vdisc_raymarch.argtypes = [vp, C.c_int, _pd, _pd, _pd, C.c_int, _pd, _u64p]
@@ -211,3 +225,75 @@ def vdisc_raymarch(desc, obj: int, ro, rd, freq=(1.0, 1.0, 0.0), cached=True):
                                       _dp(np.asarray(rd, np.float64)), _dp(np.asarray(freq, np.float64)),
                                       1 if cached else 0, _dp(out), C.byref(n))
     return err, out, n.value
+
+
+# ---- geometry probes (the reference's unit tests, tests/test_reference_kats.py) ----
+def _v(x, n=4):
+    return np.ascontiguousarray(x, np.float64).reshape(n)
+
+
+def should_stop(desc, y, i):
+    return lib().oracle_should_stop(_addr(desc), _dp(_v(y, 8)), i)
+
+
+def inside_horizon(desc, pos):
+    return bool(lib().oracle_inside_horizon(_addr(desc), _dp(_v(pos))))
+
+
+def radial_coordinate(desc, pos, cartesian=False):
+    return lib().oracle_radial_coordinate(_addr(desc), _dp(_v(pos)), 1 if cartesian else 0)
+
+
+def to_cartesian(desc, pos):
+    out = np.zeros(4)
+    lib().oracle_to_cartesian(_addr(desc), _dp(_v(pos)), _dp(out))
+    return out
+
+
+def stationary_velocity(desc, pos):
+    out = np.zeros(4)
+    lib().oracle_stationary_velocity(_addr(desc), _dp(_v(pos)), _dp(out))
+    return out
+
+
+def circular_orbit_velocity(desc, pos):
+    out = np.zeros(4)
+    err = lib().oracle_circular_orbit_velocity(_addr(desc), _dp(_v(pos)), _dp(out))
+    return err, out
+
+
+def geodesic_rhs(desc, pos, mom, y=None):
+    """(initial state y0, RHS at y (default y0), momentum_from_state at y) of the ray's solver."""
+    y0, rhs, p = np.zeros(8), np.zeros(8), np.zeros(4)
+    yi = None if y is None else _v(y, 8)
+    lib().oracle_geodesic_rhs(_addr(desc), _dp(_v(pos)), _dp(_v(mom)), _dp(yi) if yi is not None else None,
+                              _dp(y0), _dp(rhs), _dp(p))
+    return y0, rhs, p
+
+
+def ks_metric(radius, a, x, y, z, contravariant=False):
+    g = np.zeros(16)
+    lib().oracle_ks_metric(radius, a, x, y, z, 1 if contravariant else 0, _dp(g))
+    return g.reshape(4, 4)
+
+
+def bl_metric(r_s, a, r, theta):
+    g = np.zeros(16)
+    lib().oracle_bl_metric(r_s, a, r, theta, _dp(g))
+    return g.reshape(4, 4)
+
+
+def redshift_static(desc, pos, mom, observer_energy):
+    return lib().oracle_redshift_static(_addr(desc), _dp(_v(pos)), _dp(_v(mom)), observer_energy)
+
+
+def should_supersample_pair(p, pc, q, qc, adaptive, min_lum):
+    return bool(lib().oracle_should_supersample_pair(_dp(_v(p)), pc, _dp(_v(q)), qc,
+                                                     C.cast(C.pointer(adaptive), C.c_void_p), min_lum))
+
+
+def kerr_bl_rhs(r_s, a, e, l_z, q, y):
+    out = np.zeros(8)
+    lib().oracle_kerr_bl_rhs(r_s, a, e, l_z, q, _dp(_v(y, 8)), _dp(out))
+    return out
+
