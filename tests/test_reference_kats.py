@@ -500,3 +500,172 @@ def test_visible_object_contrast_triggers_supersampling(grt, oracle):  # raytrac
 def test_faint_object_contrast_does_not_trigger_supersampling(grt, oracle):  # raytracer.rs:604-618
     c = config(grt, lc=0.0, oc=0.0)
     assert not oracle.should_supersample_pair(sample(1.0, 0.0), HIT, sample(0.0, 1.0), HIT, c, 1.0)
+
+
+# ------------------------------------------------- camera tetrads (host grt_camera_build) --
+EPS = 2.220446049250313e-16  # approx::assert_abs_diff_eq! default
+
+
+def boosted_tetrad(grt, geometry, radius, a, position, velocity):
+    """Camera::new with zero rotations = lorentz_transform_tetrad(get_tetrad_at(x), u)
+    (camera.rs:151-196), by the product host code; rows of e_t, e_x, e_y, e_z."""
+    cam = grt.build_camera(geometry, radius, a, position, velocity, PI / 2, 11, 11)
+    return np.array([[cam.tetrad[i][k] for k in range(4)] for i in range(4)])
+
+
+def check_boosted_tetrad(grt, oracle, geometry, radius, position, velocity, null_eps):
+    d = desc(grt, geometry, radius=radius, objects=False)
+    t = boosted_tetrad(grt, geometry, radius, 0.0, position, velocity)
+    k = t[0] + (-t[3])
+    assert abs(oracle.inner_product(d, position, k, k)) <= null_eps
+    assert close(t[0], velocity, 1e-6)
+    for i in range(4):
+        for j in range(i + 1, 4):
+            assert abs(oracle.inner_product(d, position, t[i], t[j])) <= EPS, (i, j)
+
+
+def test_schwarzschild_lorentz_transformed_tetrad_orthonormal(grt, oracle):  # schwarzschild.rs:444-483
+    position = grt.cartesian_to_spherical((2.0, 3.0, 4.0, 5.0))
+    radius, r = 2.0, None
+    r = position[1]
+    a = 1.0 - radius / r
+    check_boosted_tetrad(grt, oracle, 1, radius, position, (1.0 / a, -math.sqrt(radius / r), 0.0, 0.0), 1e-10)
+
+
+def test_kerr_lorentz_transformed_tetrad_orthonormal(grt, oracle):  # kerr.rs:592-630
+    position = (2.0, 3.0, 4.0, 5.0)
+    radius = 2.0
+    d = desc(grt, 2, radius=radius, objects=False)
+    r = oracle.radial_coordinate(d, position)
+    a = 1.0 - radius / r
+    check_boosted_tetrad(grt, oracle, 2, radius, position, (1.0 / math.sqrt(a), 0.0, 0.0, 0.0), 1e-8)
+
+
+def test_kerr_bl_camera_tetrad_orthonormal(grt, oracle):  # kerr_bl.rs:1036-1095 (after the boost)
+    a = 0.5
+    d = desc(grt, 3, radius=1.0, a=a, objects=False)
+    pos = (0.0, 5.0, 1.2, 0.8)
+    for vel in (grt.stationary_velocity(3, 1.0, a, pos), zamo_velocity(3, 1.0, a, pos)):
+        cam = grt.build_camera(3, 1.0, a, pos, vel, PI / 2, 11, 11)
+        t = np.array([[cam.tetrad[i][k] for k in range(4)] for i in range(4)])
+        want = np.diag([-1.0, 1.0, 1.0, 1.0])
+        for i in range(4):
+            for j in range(i, 4):
+                assert abs(oracle.inner_product(d, pos, t[i], t[j]) - want[i, j]) <= 1e-10, (i, j)
+
+
+def zamo_velocity(geometry, r_s, a, pos):
+    from gr_raytracer_amd import _lib as L
+
+    out, p = np.zeros(4), np.ascontiguousarray(pos, np.float64)
+    L.check(L.lib().grt_zamo_velocity(geometry, r_s, a, L.dptr(p), L.dptr(out)), "grt_zamo_velocity")
+    return out
+
+
+def test_kerr_bl_observer_velocities_normalized(grt, oracle):  # kerr_bl.rs:1096-1125
+    a = 0.5
+    d = desc(grt, 3, radius=1.0, a=a, objects=False)
+    pos = (0.0, 5.0, 1.2, 0.0)
+    stat = grt.stationary_velocity(3, 1.0, a, pos)
+    assert abs(oracle.inner_product(d, pos, stat, stat) + 1.0) <= 1e-10
+    assert stat[3] == 0.0
+    assert close(stat, oracle.stationary_velocity(d, pos), 0.0)  # host == oracle, bit for bit
+    z = zamo_velocity(3, 1.0, a, pos)
+    assert abs(oracle.inner_product(d, pos, z, z) + 1.0) <= 1e-10
+    assert abs(oracle.inner_product(d, pos, z, (0.0, 0.0, 0.0, 1.0))) <= 1e-10
+
+
+# ------------------------------------------------ configuration.rs (host TOML loader) --
+def _load(grt, tmp_path, text, name="scene.toml"):
+    from conftest import RESOURCES
+
+    p = tmp_path / name
+    p.write_text(text)
+    return grt.HostScene(str(p), grt.GlobalOpts(camera_position=(18.0, 0.0, 0.8)), str(RESOURCES))
+
+
+def _with_adaptive(body):
+    from conftest import SCENES
+
+    return (SCENES / "euclidean.toml").read_text() + "\n[adaptive_sampling]\n" + body + "\n"
+
+
+def test_adaptive_sampling_partial_config_uses_defaults(grt, tmp_path):  # configuration.rs:238-249
+    ad = _load(grt, tmp_path, _with_adaptive("samples_per_axis = 2")).adaptive
+    want = grt.default_adaptive()
+    want.samples_per_axis = 2
+    for f, _ in ad._fields_:
+        assert getattr(ad, f) == getattr(want, f), f
+
+
+def test_adaptive_sampling_accepts_boundary_values(grt, tmp_path):  # configuration.rs:251-262
+    ad = _load(grt, tmp_path, _with_adaptive("luminance_contrast_threshold = 0.0\nopacity_contrast_threshold = 1.0\n"
+                                             "minimum_luminance = 0.0\nobject_hit_opacity_threshold = 1.0")).adaptive
+    assert (ad.luminance_contrast_threshold, ad.opacity_contrast_threshold, ad.has_minimum_luminance,
+            ad.minimum_luminance, ad.object_hit_opacity_threshold) == (0.0, 1.0, 1, 0.0, 1.0)
+
+
+@pytest.mark.parametrize("body", [  # configuration.rs:264-300
+    "samples_per_axis = 0", "luminance_contrast_threshold = -0.1", "luminance_contrast_threshold = nan",
+    "opacity_contrast_threshold = 1.1", "object_hit_opacity_threshold = inf", "minimum_luminance = -0.1",
+    "minimum_luminance = inf",
+])
+def test_adaptive_sampling_rejects_invalid_values(grt, tmp_path, body):
+    with pytest.raises(grt.GrtError):
+        _load(grt, tmp_path, _with_adaptive(body))
+
+
+DESERIALIZE = """
+celestial_temperature = 1500.0
+
+[celestial_texture.Bitmap]
+beaming_exponent = 3.0
+path = "resources/celestial.png"
+
+[geometry_type.Schwarzschild]
+radius = 2.0
+horizon_epsilon = 1e-4
+
+[[objects]]
+
+[objects.Sphere]
+radius = 1.0
+position = [1.1, 2.2, 3.3]
+temperature = 5500.0
+
+[objects.Sphere.texture.Bitmap]
+beaming_exponent = 3.0
+path = "resources/sphere.png"
+
+[[objects]]
+
+[objects.Disc]
+inner_radius = 1.0
+outer_radius = 3.0
+temperature = 6500.0
+
+[objects.Disc.texture.Checker]
+beaming_exponent = 3.0
+width = 0.5
+height = 0.5
+color1 = [255, 0, 0]
+color2 = [0, 0, 255]
+"""
+
+
+def test_deserialize(grt, tmp_path):  # configuration.rs:362-453 (texture files: the vendored ones)
+    from gr_raytracer_amd import _lib as L
+
+    hs = _load(grt, tmp_path, DESERIALIZE)  # keeps the descriptor's storage alive
+    d = hs.desc
+    assert (d.geometry, d.radius, d.horizon_epsilon, d.celestial_temperature) == (L.GEOM_SCHWARZSCHILD, 2.0, 1e-4, 1500.0)
+    assert (d.celestial.kind, d.celestial.beaming_exponent) == (L.TEX_BITMAP, 3.0)
+    assert d.n_objects == 2
+    s, k = d.objects[0], d.objects[1]
+    assert (s.kind, s.radius, tuple(s.center), s.temperature) == (L.OBJ_SPHERE, 1.0, (1.1, 2.2, 3.3), 5500.0)
+    assert (s.texture.kind, s.texture.beaming_exponent) == (L.TEX_BITMAP, 3.0)
+    assert (k.kind, k.inner_radius, k.outer_radius) == (L.OBJ_DISC, 1.0, 3.0)
+    assert (k.texture.kind, k.texture.checker_width, k.texture.checker_height) == (L.TEX_CHECKER, 0.5, 0.5)
+    # temperature 6500 feeds KerrTemperatureComputer::new: outer_radius 3 <= r_isco 6 is
+    # clamped to r_isco + 1e-6 (temperature.rs:52-58)
+    assert k.r_isco == 6.0 and k.lut_n == 1000
