@@ -669,3 +669,87 @@ def test_deserialize(grt, tmp_path):  # configuration.rs:362-453 (texture files:
     # temperature 6500 feeds KerrTemperatureComputer::new: outer_radius 3 <= r_isco 6 is
     # clamped to r_isco + 1e-6 (temperature.rs:52-58)
     assert k.r_isco == 6.0 and k.lut_n == 1000
+
+
+# ------------------------------------------------ point.rs / coordinate helpers / cli.rs --
+def test_boyer_lindquist_to_cartesian(grt, oracle):  # point.rs:221-252
+    d0 = desc(grt, 3, radius=1.0, a=0.0, objects=False)
+    ds = desc(grt, 1, radius=1.0, objects=False)
+    assert close(oracle.to_cartesian(d0, (0.0, 5.0, 1.2, 0.8)), oracle.to_cartesian(ds, (0.0, 5.0, 1.2, 0.8)), 1e-12)
+    d = desc(grt, 3, radius=1.0, a=0.5, objects=False)
+    c = oracle.to_cartesian(d, (0.0, 5.0, 1.2, 0.8))
+    assert close(c[1:], (2.91248746519832302226, 3.66769851865865170737, 1.81178877238336810684), 1e-10)
+
+
+def test_cartesian_to_spherical_round_trip(grt, oracle):  # spherical_coordinates_helper.rs:71-83
+    sph = grt.cartesian_to_spherical((0.0, 1.0, 2.0, 3.0))  # host (product) conversion
+    back = oracle.to_cartesian(desc(grt, 1, radius=1.0, objects=False), sph)
+    assert close(back, (0.0, 1.0, 2.0, 3.0), 1e-15)
+
+
+def test_parses_sampling_mask_options():  # cli.rs:121-140 (the multi-GPU render command's parser)
+    from gr_raytracer_amd.render_dist import parse_args
+
+    a = parse_args(["--show-sampling-mask", "--sampling-mask-color", "12,34,56", "--config-file", "scene.toml",
+                    "render"])
+    assert a.show_sampling_mask and a.sampling_mask_color == [12, 34, 56]
+
+
+# ------------------------------------------------------ texture.rs / color.rs / camera.rs --
+def blackbody_scene(grt, beaming):
+    b = grt.SceneBuilder(0)
+    b.integration(100, 100.0, 0.01, 1e-5)
+    b.celestial(grt.BlackBody(beaming), 0.0)
+    return b.build()
+
+
+def rel_close(a, b, rel):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.all(np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b)))
+
+
+def test_blackbody_xyz_z_one_matches_lut_sample(grt, oracle):  # texture.rs:401-412
+    d = blackbody_scene(grt, 0.0)
+    for t in (1000.0, 5000.0, 10000.0):
+        # blackbody_xyz(T, 1) = sample_blackbody(T * 1): the celestial BlackBody texture at z = 1
+        assert rel_close(oracle.texture_color(d, -1, 0.0, 0.0, 1.0, t)[:3],
+                         oracle.texture_color(d, -1, 0.0, 0.0, 1.0, t * 1.0)[:3], 1e-12)
+
+
+def test_blackbody_xyz_relativistic_boost(grt, oracle):  # texture.rs:414-429
+    d = blackbody_scene(grt, 0.0)
+    base = oracle.texture_color(d, -1, 0.0, 0.0, 1.0, 6000.0)
+    boosted = oracle.texture_color(d, -1, 0.0, 0.0, 2.0, 6000.0)
+    assert np.all(boosted[:3] > base[:3])
+
+
+def test_blackbody_beaming_exponent(grt, oracle):  # texture.rs:431-474
+    d0, d4 = blackbody_scene(grt, 0.0), blackbody_scene(grt, 4.0)
+    base = oracle.texture_color(d0, -1, 0.0, 0.0, 1.5, 6000.0)        # blackbody_xyz(6000, 1.5)
+    assert rel_close(base[:3], oracle.texture_color(d0, -1, 0.0, 0.0, 1.0, 9000.0)[:3], 1e-12)
+    rendered = oracle.texture_color(d4, -1, 0.0, 0.0, 1.5, 6000.0)
+    assert rel_close(rendered[:3], base[:3] * math.pow(1.5, 4.0), 1e-12)
+    assert rendered[0] != base[0]
+
+
+def test_srgb_to_xyz_round_trip(grt):  # color.rs:339-350 (host grt_srgb_to_xyza / grt_xyz_to_srgb)
+    from gr_raytracer_amd import _lib as L
+
+    c = grt.srgb_to_xyza(255, 42, 10, 255)
+    out = np.zeros(3, np.uint8)
+    L.lib().grt_xyz_to_srgb(L.dptr(np.ascontiguousarray(c[:3])), 1.0, L.ptr(out, L.C.c_uint8))
+    assert tuple(out) == (255, 42, 10) and c[3] == 1.0
+
+
+@pytest.mark.parametrize("geometry,radius", [(4, 0.0), (1, 0.0)])
+def test_get_ray_for_different_geometries(grt, oracle, geometry, radius):  # camera.rs:366-460
+    """A spherical-chart camera (EuclideanSpherical, Schwarzschild r_s = 0) at the
+    Cartesian camera's position: every pixel's ray starts at the same point."""
+    pos = (0.0, 0.0, 1.0, 0.0)
+    cart = grt.build_camera(0, 0.0, 0.0, pos, (1.0, 0.0, 0.0, 0.0), PI / 2, 100, 100, 0.0, PI / 2, PI / 2)
+    sph_pos = grt.cartesian_to_spherical(pos)
+    sph = grt.build_camera(geometry, radius, 0.0, sph_pos, (1.0, 0.0, 0.0, 0.0), PI / 2, 100, 100, 0.0, PI / 2,
+                           PI / 2)
+    d = desc(grt, geometry, radius=radius, horizon=0.0, objects=False)
+    back = oracle.to_cartesian(d, [sph.position[k] for k in range(4)])
+    assert close([cart.position[k] for k in range(4)], back, 1e-10)
