@@ -219,15 +219,15 @@ def test_render_dist_two_ranks_equal_grt_cli(gpu, tone):
     with tempfile.TemporaryDirectory() as d:
         ref_png, ref_raw = os.path.join(d, "ref.png"), os.path.join(d, "ref.raw")
         subprocess.run([str(ROOT / "gr_raytracer_amd" / "lib" / "grt"), *flags, "--raw-out", ref_raw, "render",
-                        "--filename", ref_png], check=True, timeout=100, env=env)
+                        "--filename", ref_png], check=True, timeout=240, env=env)
         png, raw, png2 = os.path.join(d, "d.png"), os.path.join(d, "d.raw"), os.path.join(d, "d2.png")
         launch = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                   "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "gr_raytracer_amd.render_dist",
                   "--backend=gloo", "--band-rows=8"]
-        subprocess.run([*launch, *flags, "--raw-out", raw, "render", "--filename", png], check=True, timeout=100,
+        subprocess.run([*launch, *flags, "--raw-out", raw, "render", "--filename", png], check=True, timeout=240,
                        env=env, cwd=str(ROOT))
         launch[5] = f"--master-port={_free_port()}"
-        subprocess.run([*launch, *flags, "render", "--filename", png2], check=True, timeout=100, env=env,
+        subprocess.run([*launch, *flags, "render", "--filename", png2], check=True, timeout=240, env=env,
                        cwd=str(ROOT))
         assert np.array_equal(np.fromfile(raw), np.fromfile(ref_raw))
         ref = open(ref_png, "rb").read()
