@@ -208,11 +208,12 @@ def test_shard_sampling_mask_equals_render_section(grt, gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tone", ["reinhard", "global-linear"])
-def test_render_dist_two_ranks_equal_grt_cli(gpu, tone):
-    """`render_dist` with 2 ranks (gloo, both on GPU 0) writes the same PNG and the same
-    f64 frame as the single-GPU `grt` binary; the stock TOML supersamples adaptively."""
-    flags = ["--width=80", "--height=72", "--camera-position=-16.0,0.0,3.5", "--theta=-3.142",
+@pytest.mark.parametrize("tone,ranks,height", [("reinhard", 2, 72), ("global-linear", 2, 72),
+                                               ("reinhard", 3, 80)])  # 10 bands of 8 over 3 ranks: 4 / 3 / 3
+def test_render_dist_ranks_equal_grt_cli(gpu, tone, ranks, height):
+    """`render_dist` with 2 or 3 ranks (gloo, all on GPU 0) writes the same PNG and the
+    same f64 frame as the single-GPU `grt` binary; the stock TOML supersamples adaptively."""
+    flags = ["--width=80", f"--height={height}", "--camera-position=-16.0,0.0,3.5", "--theta=-3.142",
              "--max-steps=100000", f"--tone-mapping={tone}", "--config-file", str(SCENES / "schwarzschild.toml"),
              "--resource-root", str(RESOURCES)]
     env = dict(os.environ, PYTHONPATH=str(ROOT))
@@ -221,7 +222,7 @@ def test_render_dist_two_ranks_equal_grt_cli(gpu, tone):
         subprocess.run([str(ROOT / "gr_raytracer_amd" / "lib" / "grt"), *flags, "--raw-out", ref_raw, "render",
                         "--filename", ref_png], check=True, timeout=240, env=env)
         png, raw, png2 = os.path.join(d, "d.png"), os.path.join(d, "d.raw"), os.path.join(d, "d2.png")
-        launch = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+        launch = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
                   "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "gr_raytracer_amd.render_dist",
                   "--backend=gloo", "--band-rows=8"]
         subprocess.run([*launch, *flags, "--raw-out", raw, "render", "--filename", png], check=True, timeout=240,
