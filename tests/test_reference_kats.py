@@ -753,3 +753,39 @@ def test_get_ray_for_different_geometries(grt, oracle, geometry, radius):  # cam
     d = desc(grt, geometry, radius=radius, horizon=0.0, objects=False)
     back = oracle.to_cartesian(d, [sph.position[k] for k in range(4)])
     assert close([cart.position[k] for k in range(4)], back, 1e-10)
+
+
+# ----------------------------------------------------- kerr_bl.rs: chart consistency --
+def test_e_lz_consistency_between_ks_and_bl(grt, oracle):  # kerr_bl.rs:930-1034
+    a = 0.5
+    dk, pk, mk, db, pb, mb = ks_camera_ray(grt, oracle, a, 5, 8)
+    y0, _, p = oracle.geodesic_rhs(db, pb, mb)  # Cartesian ray -> BL state (via the Jacobian)
+    e_cart, _, _ = constants_of_motion(oracle, a, y0[:4], p)
+    assert -2.0 < e_cart < -0.5
+    y1, _, p1 = oracle.geodesic_rhs(db, y0[:4], p)  # the same ray, entering as a BL ray
+    e_bl, lz_bl, _ = constants_of_motion(oracle, a, y1[:4], p1)
+    assert -2.0 < e_bl < -0.5 and math.isfinite(lz_bl)
+    assert abs(e_cart - e_bl) <= 1e-10
+    pc = oracle.ks_metric(1.0, a, pk[1], pk[2], pk[3]) @ mk  # Kerr::get_constants_of_motion
+    kerr_e = -pc[0]
+    kerr_lz = pc[1] * (-pk[2]) + pc[2] * pk[1]
+    assert abs(kerr_e - e_cart) <= 1e-10
+    assert abs(kerr_lz - lz_bl) <= 1e-10
+
+
+def test_redshift_agreement_schwarzschild_limit(grt, oracle):  # kerr_bl.rs:1452-1573
+    _, _, _, db, pb, mb = ks_camera_ray(grt, oracle, 0.0, 3, 7)
+    tb, _, _ = oracle.integrate_ray(db, pb, mb)
+    pos_s = grt.cartesian_to_spherical((0.0, -10.0, 0.0, 2.0))
+    vel_s = (1.0 / math.sqrt(1.0 - 1.0 / pos_s[1]), 0.0, 0.0, 0.0)
+    ds = desc(grt, 1, radius=1.0, horizon=1e-5, camera=(pos_s, vel_s, PI / 2, 11, 11), epsilon=1e-6)
+    ms = oracle.camera_ray(ds, 3, 7)
+    ts, _, _ = oracle.integrate_ray(ds, pos_s, ms)
+    assert len(tb) > 2 and len(ts) > 2
+    r_bl = tb[0, 2]
+    vel_bl = (1.0 / math.sqrt(1.0 - 1.0 / r_bl), 0.0, 0.0, 0.0)
+    obs_bl = oracle.inner_product(db, tb[0, 1:5], vel_bl, tb[0, 5:9])
+    obs_s = oracle.inner_product(ds, pos_s, vel_s, ms)
+    g_bl = oracle.redshift_static(db, tb[-1, 1:5], tb[-1, 5:9], obs_bl)
+    g_s = oracle.redshift_static(ds, ts[-1, 1:5], ts[-1, 5:9], obs_s)
+    assert abs(g_bl - g_s) <= 0.01
