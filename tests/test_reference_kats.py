@@ -789,3 +789,18 @@ def test_redshift_agreement_schwarzschild_limit(grt, oracle):  # kerr_bl.rs:1452
     g_bl = oracle.redshift_static(db, tb[-1, 1:5], tb[-1, 5:9], obs_bl)
     g_s = oracle.redshift_static(ds, ts[-1, 1:5], ts[-1, 5:9], obs_s)
     assert abs(g_bl - g_s) <= 0.01
+
+
+def test_schwarzschild_and_kerr_ray_null(grt, oracle):  # schwarzschild.rs:511-537, kerr.rs:656-683
+    pos = grt.cartesian_to_spherical((2.0, 3.0, 4.0, 5.0))
+    a = 1.0 - 2.0 / pos[1]
+    d = desc(grt, 1, radius=2.0, camera=(pos, (1.0 / a, -math.sqrt(2.0 / pos[1]), 0.0, 0.0), PI / 2, 11, 11))
+    m = oracle.camera_ray(d, 1, 6)
+    assert abs(oracle.inner_product(d, pos, m, m)) <= 1e-10
+    pk = (2.0, 3.0, 4.0, 5.0)
+    dk0 = desc(grt, 2, radius=2.0, objects=False)
+    ak = 1.0 - 2.0 / oracle.radial_coordinate(dk0, pk)
+    dk = desc(grt, 2, radius=2.0, camera=(pk, (1.0 / math.sqrt(ak), 0.0, 0.0, 0.0), PI / 2, 11, 11, 0.0, PI / 2,
+                                          PI / 2))
+    mk = oracle.camera_ray(dk, 1, 6)
+    assert abs(oracle.inner_product(dk, pk, mk, mk)) <= 1e-8
