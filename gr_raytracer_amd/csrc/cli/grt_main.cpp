@@ -45,6 +45,28 @@ static int usage(const char* msg) {
   return 2;
 }
 
+// impl FromStr for Color (color.rs:151-170): three comma-separated components, each
+// trimmed and parsed as u8 (optional '+', decimal digits, at most 255).
+static bool parse_rgb(const std::string& s, uint8_t out[3]) {
+  int n = 0;
+  size_t p = 0;
+  while (true) {
+    size_t q = s.find(',', p);
+    std::string tok = s.substr(p, q == std::string::npos ? std::string::npos : q - p);
+    size_t b = tok.find_first_not_of(" \t\n\r\f\v"), e = tok.find_last_not_of(" \t\n\r\f\v");
+    if (b == std::string::npos) return false;
+    tok = tok.substr(b, e - b + 1);
+    if (tok[0] == '+') tok = tok.substr(1);
+    if (tok.empty() || tok.size() > 3 || tok.find_first_not_of("0123456789") != std::string::npos) return false;
+    int v = std::atoi(tok.c_str());
+    if (v > 255 || n >= 3) return false;
+    out[n++] = (uint8_t)v;
+    if (q == std::string::npos) break;
+    p = q + 1;
+  }
+  return n == 3;
+}
+
 static bool split_csv(const std::string& s, std::vector<double>& out) {
   out.clear();
   size_t p = 0;
@@ -196,11 +218,9 @@ int main(int argc, char** argv) {
       else if (v == "global-linear") opts.tone_mapping = GRT_TONE_GLOBAL_LINEAR;
       else return usage("tone mapping must be reinhard or global-linear");
     } else if (a == "--sampling-mask-color") {
-      if (!split_csv(v, nums) || nums.size() != 3) return usage("invalid RGB color; expected R,G,B");
-      for (int k = 0; k < 3; ++k) {
-        if (nums[k] < 0 || nums[k] > 255 || nums[k] != std::floor(nums[k])) return usage("invalid RGB color");
-        opts.sampling_mask_color[k] = (uint8_t)nums[k];
-      }
+      uint8_t rgb[3];
+      if (!parse_rgb(v, rgb)) return usage(("invalid RGB color '" + v + "'; expected R,G,B").c_str());
+      for (int k = 0; k < 3; ++k) opts.sampling_mask_color[k] = rgb[k];
     } else if (a == "-c" || a == "--config-file") config_file = v;
     else return usage(("unknown argument " + a).c_str());
   }

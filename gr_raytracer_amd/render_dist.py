@@ -34,6 +34,21 @@ def _csv(n: int, conv=float):
     return parse
 
 
+def _rgb(v: str):
+    """impl FromStr for Color (color.rs:151-170): three trimmed u8 components."""
+    parts = v.split(",")
+    out = []
+    for part in parts:
+        t = part.strip()
+        t = t[1:] if t.startswith("+") else t
+        if not t or not t.isdigit() or not t.isascii() or int(t) > 255:
+            raise argparse.ArgumentTypeError(f"invalid RGB color '{v}'; expected three values from 0 to 255")
+        out.append(int(t))
+    if len(out) != 3:
+        raise argparse.ArgumentTypeError(f"invalid RGB color '{v}'; expected R,G,B (for example 255,0,255)")
+    return out
+
+
 def parse_args(argv):
     """cli.rs:5-113 for `render`: global options anywhere, then the subcommand."""
     p = argparse.ArgumentParser(prog="render_dist", description=__doc__.splitlines()[0])
@@ -49,7 +64,7 @@ def parse_args(argv):
     p.add_argument("--psi", type=float, default=0.0)
     p.add_argument("--tone-mapping", choices=["reinhard", "global-linear"], default="reinhard")
     p.add_argument("--show-sampling-mask", action="store_true")
-    p.add_argument("--sampling-mask-color", type=_csv(3, int), default=[255, 0, 255])
+    p.add_argument("--sampling-mask-color", type=_rgb, default=[255, 0, 255])
     p.add_argument("-c", "--config-file", required=True)
     p.add_argument("--resource-root", default=None)
     p.add_argument("--raw-out", default=None)
@@ -62,9 +77,6 @@ def parse_args(argv):
     a = p.parse_args(argv)
     if any(getattr(a, f[2:].replace("-", "_")) is not None for f in RENDER_FLAGS[1:]):
         p.error("sections (--from-row/--from-col/--to-row/--to-col) are single-GPU only: use grt")
-    for k in a.sampling_mask_color:
-        if not 0 <= k <= 255:
-            p.error("invalid RGB color; expected R,G,B")
     return a
 
 

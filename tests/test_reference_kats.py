@@ -804,3 +804,37 @@ def test_schwarzschild_and_kerr_ray_null(grt, oracle):  # schwarzschild.rs:511-5
                                           PI / 2))
     mk = oracle.camera_ray(dk, 1, 6)
     assert abs(oracle.inner_product(dk, pk, mk, mk)) <= 1e-8
+
+
+# ------------------------------------------------------------ color.rs: RGB parsing --
+RGB_OK = {" 12, 34 ,56 ": [12, 34, 56]}                          # color.rs:352-358
+RGB_BAD = ["12,34", "12,34,56,78", "12,blue,56", "12,34,256"]    # color.rs:360-368
+
+
+def test_rgb_color_parsing_render_dist():
+    import argparse
+
+    from gr_raytracer_amd.render_dist import _rgb
+
+    for v, want in RGB_OK.items():
+        assert _rgb(v) == want
+    for v in RGB_BAD:
+        with pytest.raises(argparse.ArgumentTypeError):
+            _rgb(v)
+
+
+def test_rgb_color_parsing_grt_cli(tmp_path):
+    import subprocess
+
+    from conftest import ROOT
+
+    grt_bin = str(ROOT / "gr_raytracer_amd" / "lib" / "grt")
+    missing = str(tmp_path / "missing.toml")  # parsing happens first; an accepted colour fails on the file
+    for v in RGB_OK:
+        r = subprocess.run([grt_bin, "--sampling-mask-color", v, "--config-file", missing, "render"],
+                           capture_output=True, text=True, timeout=60)
+        assert "Config file not found" in r.stderr, r.stderr
+    for v in RGB_BAD:
+        r = subprocess.run([grt_bin, "--sampling-mask-color", v, "--config-file", missing, "render"],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode != 0 and "invalid RGB color" in r.stderr, r.stderr
