@@ -18,6 +18,9 @@
 // resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer.
 #include <chrono>
 #include <cmath>
+#include <cstdint>
+#include <cctype>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +46,25 @@ static int usage(const char* msg) {
                "           [--min-redshift Z] [--max-redshift Z] [--width N] [--height N] [-f FILE]\n",
                msg);
   return 2;
+}
+
+// clap's value parsers for the flag types of cli.rs:5-113: the whole string must be a
+// number of the field's type (f64 / i64 / u32 / usize); anything else is an error.
+static bool parse_f64(const std::string& v, double* out) {
+  if (v.empty() || std::isspace((unsigned char)v[0])) return false;
+  char* end = nullptr;
+  *out = std::strtod(v.c_str(), &end);
+  return *end == 0;
+}
+static bool parse_i64(const std::string& v, long long lo, unsigned long long hi, long long* out) {
+  if (v.empty() || std::isspace((unsigned char)v[0])) return false;
+  const bool neg = v[0] == '-';
+  const std::string d = (v[0] == '+' || neg) ? v.substr(1) : v;
+  if (d.empty() || d.find_first_not_of("0123456789") != std::string::npos || d.size() > 19) return false;
+  const unsigned long long m = std::strtoull(d.c_str(), nullptr, 10);
+  if (neg ? (lo >= 0 ? m != 0 : m > (unsigned long long)(-(lo + 1)) + 1) : m > hi) return false;
+  *out = neg ? -(long long)(m - 1) - 1 : (long long)m;
+  return true;
 }
 
 // impl FromStr for Color (color.rs:151-170): three comma-separated components, each
@@ -169,18 +191,28 @@ int main(int argc, char** argv) {
     if (action.empty() && a == "--show-sampling-mask") { opts.show_sampling_mask = 1; continue; }
     if (!next(v)) return usage(("missing value for " + a).c_str());
     std::vector<double> nums;
+    auto bad = [&]() { return usage(("invalid value '" + v + "' for '" + a + "'").c_str()); };
+    auto f64 = [&](double* out) { return parse_f64(v, out); };
+    auto int_in = [&](long long lo, unsigned long long hi, long long* out) { return parse_i64(v, lo, hi, out); };
+    long long iv = 0;
     // extras accepted anywhere
     if (a == "--device") { device = std::atoi(v.c_str()); continue; }
     if (a == "--resource-root") { resource_root = v; continue; }
     if (a == "--raw-out") { raw_out = v; continue; }
     if (!action.empty()) {  // subcommand options
       if (a == "--filename") filename = v;
-      else if (action == "render" && a == "--from-row") from_row = std::atol(v.c_str());
-      else if (action == "render" && a == "--from-col") from_col = std::atol(v.c_str());
-      else if (action == "render" && a == "--to-row") to_row = std::atol(v.c_str());
-      else if (action == "render" && a == "--to-col") to_col = std::atol(v.c_str());
-      else if (action == "render-ray" && (a == "-r" || a == "--row")) { ray_row = std::atoll(v.c_str()); have_row = true; }
-      else if (action == "render-ray" && (a == "-c" || a == "--col")) { ray_col = std::atoll(v.c_str()); have_col = true; }
+      else if (action == "render" && (a == "--from-row" || a == "--from-col" || a == "--to-row" || a == "--to-col")) {
+        if (!int_in(0, 4294967295ull, &iv)) return bad();  // Option<u32>
+        (a == "--from-row" ? from_row : a == "--from-col" ? from_col : a == "--to-row" ? to_row : to_col) = (long)iv;
+      } else if (action == "render-ray" && (a == "-r" || a == "--row")) {
+        if (!int_in(INT64_MIN, INT64_MAX, &iv)) return bad();  // i64
+        ray_row = iv;
+        have_row = true;
+      } else if (action == "render-ray" && (a == "-c" || a == "--col")) {
+        if (!int_in(INT64_MIN, INT64_MAX, &iv)) return bad();
+        ray_col = iv;
+        have_col = true;
+      }
       else if (action == "render-ray-at" && (a == "-p" || a == "--position")) {
         if (!split_csv(v, ray_position)) return usage("invalid position");
         have_position = true;
@@ -188,28 +220,41 @@ int main(int argc, char** argv) {
         if (!split_csv(v, ray_direction)) return usage("invalid direction");
         have_direction = true;
       } else if (action == "blackbody" && (a == "-t" || a == "--temperature")) {
-        bb_temperature = std::atof(v.c_str());
+        if (!f64(&bb_temperature)) return bad();
         have_temperature = true;
-      } else if (action == "blackbody" && (a == "-r" || a == "--redshift")) bb_redshift = std::atof(v.c_str());
-      else if (action == "blackbody-spectrum" && a == "--min-temperature") bb_tmin = std::atof(v.c_str());
-      else if (action == "blackbody-spectrum" && a == "--max-temperature") bb_tmax = std::atof(v.c_str());
-      else if (action == "blackbody-spectrum" && a == "--min-redshift") bb_zmin = std::atof(v.c_str());
-      else if (action == "blackbody-spectrum" && a == "--max-redshift") bb_zmax = std::atof(v.c_str());
-      else if (action == "blackbody-spectrum" && a == "--width") bb_w = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
-      else if (action == "blackbody-spectrum" && a == "--height") bb_h = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
+      } else if (action == "blackbody" && (a == "-r" || a == "--redshift")) {
+        if (!f64(&bb_redshift)) return bad();
+      } else if (action == "blackbody-spectrum" && a == "--min-temperature") {
+        if (!f64(&bb_tmin)) return bad();
+      } else if (action == "blackbody-spectrum" && a == "--max-temperature") {
+        if (!f64(&bb_tmax)) return bad();
+      } else if (action == "blackbody-spectrum" && a == "--min-redshift") {
+        if (!f64(&bb_zmin)) return bad();
+      } else if (action == "blackbody-spectrum" && a == "--max-redshift") {
+        if (!f64(&bb_zmax)) return bad();
+      } else if (action == "blackbody-spectrum" && (a == "--width" || a == "--height")) {
+        if (!int_in(0, 4294967295ull, &iv)) return bad();  // u32
+        (a == "--width" ? bb_w : bb_h) = (uint32_t)iv;
+      }
       else if (action == "blackbody-spectrum" && a == "-f") filename = v;
       else return usage(("unknown argument " + a + " for " + action).c_str());
       continue;
     }
-    if (a == "--width") opts.width = std::atoll(v.c_str());
-    else if (a == "--height") opts.height = std::atoll(v.c_str());
-    else if (a == "--step-size") opts.step_size = std::atof(v.c_str());
-    else if (a == "--max-steps") opts.max_steps = std::strtoull(v.c_str(), nullptr, 10);
-    else if (a == "--max-radius") opts.max_radius = std::atof(v.c_str());
-    else if (a == "--epsilon") opts.epsilon = std::atof(v.c_str());
-    else if (a == "--phi") opts.phi = std::atof(v.c_str());
-    else if (a == "--theta") opts.theta = std::atof(v.c_str());
-    else if (a == "--psi") opts.psi = std::atof(v.c_str());
+    if (a == "--width" || a == "--height") {
+      if (!int_in(INT64_MIN, INT64_MAX, &iv)) return bad();  // i64
+      (a == "--width" ? opts.width : opts.height) = iv;
+    } else if (a == "--max-steps") {  // usize
+      const std::string d = (!v.empty() && v[0] == '+') ? v.substr(1) : v;
+      if (d.empty() || d.find_first_not_of("0123456789") != std::string::npos) return bad();
+      errno = 0;
+      opts.max_steps = std::strtoull(d.c_str(), nullptr, 10);
+      if (errno == ERANGE) return bad();
+    } else if (a == "--step-size") { if (!f64(&opts.step_size)) return bad(); }
+    else if (a == "--max-radius") { if (!f64(&opts.max_radius)) return bad(); }
+    else if (a == "--epsilon") { if (!f64(&opts.epsilon)) return bad(); }
+    else if (a == "--phi") { if (!f64(&opts.phi)) return bad(); }
+    else if (a == "--theta") { if (!f64(&opts.theta)) return bad(); }
+    else if (a == "--psi") { if (!f64(&opts.psi)) return bad(); }
     else if (a == "--camera-position") {
       if (!split_csv(v, nums) || nums.size() != 3) return usage("Camera position must be a vector of length 3");
       for (int k = 0; k < 3; ++k) opts.camera_position[k] = nums[k];
