@@ -173,7 +173,8 @@ def lib() -> C.CDLL:
                                         C.POINTER(AuxOut), C.POINTER(Stats)]),
         "grt_render_pixels_async": (C.c_int, [vp, C.c_int, vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp]),
         "grt_render_section": (C.c_int, [vp, C.c_int, u32, u32, u32, u32, C.POINTER(AdaptiveConfig), _pd, _pd,
-                                         C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(Stats)]),
+                                         C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(Stats),
+                                         C.POINTER(C.c_uint8)]),
         "grt_set_launch_config": (C.c_int, [C.c_int, C.c_int]),
         "grt_set_schedule": (C.c_int, [C.c_int]),
         "grt_shard_row_count": (u32, [u32, C.POINTER(RowShard)]),

@@ -48,6 +48,17 @@ static int usage(const char* msg) {
   return 2;
 }
 
+// Debug form of the RaytracerError behind a grt_status (raytracer.rs:20-52).
+static const char* error_debug_name(int status) {
+  switch (status) {
+    case GRT_ERR_MAX_STEPS_REACHED: return "IntegrationError(MaxStepsReached)";
+    case GRT_ERR_NO_CIRCULAR_ORBIT: return "NoCircularOrbitPossible";
+    case GRT_ERR_BELOW_RISCO: return "BelowRISCO";
+    case GRT_ERR_NON_FINITE_RADIUS: return "NonFiniteRadius";
+    default: return "Unknown";
+  }
+}
+
 // clap's value parsers for the flag types of cli.rs:5-113: the whole string must be a
 // number of the field's type (f64 / i64 / u32 / usize); anything else is an error.
 static bool parse_f64(const std::string& v, double* out) {
@@ -360,10 +371,18 @@ int main(int argc, char** argv) {
   }
   grt_stats st;
   uint64_t nsel = 0;
-  if (grt_render_section(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st)) {
+  std::vector<uint8_t> status((size_t)w * h);
+  if (grt_render_section(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st,
+                         status.data())) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
+  // raytracer.rs:232-239: every pixel whose color_of_ray failed is logged (Debug form of
+  // the RaytracerError) and keeps the default colour
+  for (size_t i = 0; i < status.size(); ++i)
+    if (status[i] & 0x7f)
+      std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n",
+                   (unsigned)(c0 + i % w), (unsigned)(r0 + i / w), error_debug_name(status[i] & 0x7f));
   std::fprintf(stderr, "[grt] %llu rays, %llu accepted steps, %llu attempts, %llu supersampled pixels, kernel %.1f ms "
                "(%.3e steps/s)\n",
                (unsigned long long)st.rays, (unsigned long long)st.accepted_steps, (unsigned long long)st.attempts,

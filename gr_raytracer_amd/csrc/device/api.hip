@@ -741,7 +741,8 @@ double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adapt
 
 int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
                        uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza,
-                       double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats) {
+                       double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats,
+                       uint8_t* status_out) {
   if (!s || !cfg || !xyza_out) return fail(-EINVAL, "null argument");
   if (to_row < from_row || to_col < from_col) return fail(-EINVAL, "empty section");
   if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
@@ -833,6 +834,7 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
   HIP_TRY(hipEventSynchronize(dc->ev1));
   HIP_TRY(hipMemcpy(xyza_out, b_x64.p, n * 32, hipMemcpyDeviceToHost));
   if (class_out) HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
+  if (status_out) HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
   if (n_supersampled) *n_supersampled = n_sel;
   if (stats) {
     unsigned long long hs[4];

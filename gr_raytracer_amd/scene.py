@@ -222,7 +222,8 @@ class Scene:
         L.check(L.lib().grt_render_section(self._s, device, from_row, from_col, to_row, to_col,
                                            C.byref(adaptive or self.adaptive),
                                            L.dptr(mask) if mask is not None else None, L.dptr(out),
-                                           L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st)), "grt_render_section")
+                                           L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st), None),
+                "grt_render_section")
         return out, cls, int(nsel.value), _stats_dict(st)
 
     def _trace(self, fn, a, b, width: int, capacity: int, device: int):

@@ -359,7 +359,9 @@ int grt_render_pixels_async(grt_scene* scene, int device, void* stream,
 int grt_render_section(grt_scene* scene, int device, uint32_t from_row, uint32_t from_col,
                        uint32_t to_row, uint32_t to_col, const grt_adaptive_config* cfg,
                        const double* sampling_mask_xyza, double* xyza_out,
-                       uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats);
+                       uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats,
+                       uint8_t* status_out /* nullable: grt_status of each pixel's 1-spp ray, the
+                                              error the reference logs at raytracer.rs:232-239 */);
 
 /* Row-band sharding of one frame across GPUs (multi-GPU render).
  * The frame's rows are cut into bands of `band_rows` rows (the last may be short);

@@ -234,3 +234,28 @@ def test_render_dist_ranks_equal_grt_cli(gpu, tone, ranks, height):
         ref = open(ref_png, "rb").read()
         assert open(png, "rb").read() == ref  # rank 0 tone-maps the gathered f64 frame
         assert open(png2, "rb").read() == ref  # per-rank tone mapping, sRGB rows gathered
+
+
+@pytest.mark.gpu
+def test_grt_cli_logs_failed_pixels_like_the_reference(grt, oracle, gpu, tmp_path):
+    """raytracer.rs:232-239: the `render` CLI logs every pixel whose colour failed and
+    the set equals the oracle's.  The C2 scene with its disc reaching inside the ISCO
+    (inner radius 2 < r_isco = 3): those hits fail with BelowRISCO (temperature.rs)."""
+    import re
+
+    scene = tmp_path / "below_isco.toml"
+    scene.write_text((SCENES / "schwarzschild.toml").read_text().replace("inner_radius = 3.0", "inner_radius = 2.0"))
+    flags = ["--width=64", "--height=64", "--camera-position=-16.0,0.0,3.5", "--theta=-3.142", "--max-steps=100000",
+             "--config-file", str(scene), "--resource-root", str(RESOURCES)]
+    r = subprocess.run([str(ROOT / "gr_raytracer_amd" / "lib" / "grt"), *flags, "render", "--filename",
+                        str(tmp_path / "o.png")], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    names = {1: "IntegrationError(MaxStepsReached)", 2: "NoCircularOrbitPossible", 3: "BelowRISCO",
+             4: "NonFiniteRadius"}
+    got = {(int(x), int(y), e) for x, y, e in
+           re.findall(r"Unable to compute color for ray at pixel \((\d+), (\d+)\): (\S+)", r.stderr)}
+    hs = grt.HostScene(str(scene), c2_opts(grt, width=64, height=64), str(RESOURCES))
+    ref = oracle.render_pixels(hs.desc, 0, 0, 64, 64, threads=16)
+    st = ref["status"].reshape(64, 64) & 0x7F
+    want = {(int(c), int(rw), names[int(st[rw, c])]) for rw, c in zip(*np.nonzero(st))}
+    assert len(want) > 10 and got == want
