@@ -40,6 +40,9 @@ namespace grt {
 #ifndef GRT_SHARED_DIV
 #define GRT_SHARED_DIV 1
 #endif
+#ifndef GRT_UNIT_H
+#define GRT_UNIT_H 1  // far-field attempts of a wave with h == 1 everywhere skip h * o
+#endif
 
 // f64::powf == glibc pow: bit-exact on glibc's fast path, OCML outside it.
 GDEV double rpow(double x, double y) {
@@ -390,41 +393,44 @@ struct Dim {
 
 // One rkf45_step (runge_kutta.rs:86-125).  Returns the SQUARED truncation error norm:
 // the controller takes the (correctly rounded) sqrt only when the decision needs it.
-template <int G>
+// UNIT_H: every lane of the wave has h == 1.0 (H_MAX, the far field), where h * o is o
+// itself (x * 1.0 == x for every finite and infinite x and keeps the sign of zero; a NaN
+// stays a NaN, which stops the ray either way), so the eight products per stage go.
+template <int G, bool UNIT_H = false>
 GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
                         double* yn) {
   constexpr int D = Dim<G>::D;
   double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
   rhs<G>(S, rc, y, o);
 #pragma unroll
-  for (int i = 0; i < D; ++i) k1[i] = h * o[i];
+  for (int i = 0; i < D; ++i) k1[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
   if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
   rhs<G>(S, rc, tmp, o);
 #pragma unroll
-  for (int i = 0; i < D; ++i) k2[i] = h * o[i];
+  for (int i = 0; i < D; ++i) k2[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * k1[i] + B32 * k2[i];
   rhs<G>(S, rc, tmp, o);
 #pragma unroll
-  for (int i = 0; i < D; ++i) k3[i] = h * o[i];
+  for (int i = 0; i < D; ++i) k3[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * k1[i] + B42 * k2[i] + B43 * k3[i];
   rhs<G>(S, rc, tmp, o);
 #pragma unroll
-  for (int i = 0; i < D; ++i) k4[i] = h * o[i];
+  for (int i = 0; i < D; ++i) k4[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * k1[i] + B52 * k2[i] + B53 * k3[i] + B54 * k4[i];
   rhs<G>(S, rc, tmp, o);
 #pragma unroll
-  for (int i = 0; i < D; ++i) k5[i] = h * o[i];
+  for (int i = 0; i < D; ++i) k5[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i)
     tmp[i] = y[i] + B61 * k1[i] + B62 * k2[i] + B63 * k3[i] + B64 * k4[i] + B65 * k5[i];
   rhs<G>(S, rc, tmp, o);
 #pragma unroll
-  for (int i = 0; i < D; ++i) k6[i] = h * o[i];
+  for (int i = 0; i < D; ++i) k6[i] = UNIT_H ? o[i] : h * o[i];
   double e[8];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
@@ -1145,7 +1151,12 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
 
     // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
     double yn[8];
-    const double err_sq = rkf_attempt<G>(S, rc, y, h_cur, yn);
+    // Kerr-Schild: the RHS dwarfs the saved products, and a second copy of its attempt
+    // (+80 KB of code) is not worth them
+    constexpr bool UNIT_H_COPY = GRT_UNIT_H && G != GRT_GEOM_KERR;
+    const double err_sq = (UNIT_H_COPY && __ballot(active && h_cur != 1.0) == 0)
+                              ? rkf_attempt<G, UNIT_H_COPY>(S, rc, y, h_cur, yn)
+                              : rkf_attempt<G, false>(S, rc, y, h_cur, yn);
     n_att++;
     double h_next;
     const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
