@@ -163,7 +163,7 @@ def main() -> None:
         att_per_launch = attempts / args.steps
         flop_per_launch = f_att * att_per_launch + f_step * acc_per_launch
         achieved_tflops = flop_per_launch / (kernel_ms * 1e-3) / 1e12
-        prof = ROOT / "profiles" / "r01p_pmc.json"  # PMC passes of this kernel, tools/run_pmc.sh
+        prof = ROOT / "profiles" / "r01t_pmc.json"  # PMC passes of this kernel, tools/run_pmc.sh
         traffic = None
         if prof.exists():
             try:
