@@ -26,7 +26,8 @@ namespace {
 int g_blocks_per_cu = 0;
 int g_threads = 256;
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
-constexpr uint32_t PROBE_CAP = 32768;  // > the ~1.6e4 steps of an escaping ray at H_MAX
+constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
+
 
 int fail(int code, const std::string& msg) {
   grt_host::set_error(msg);
@@ -357,6 +358,15 @@ grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_
   return wl;
 }
 
+// Step cap of the probe rays: an escaping ray needs about max_radius accepted steps at
+// H_MAX = 1 (C4: 15825-15900 steps for max_radius 15000), so 1.3 x max_radius still
+// tells them from the long rays while the capped probes (which run the whole cap) end
+// sooner: C4's probe pass 1.86 s -> ~1.2 s per 1/8 shard.  Scheduling only.
+static uint32_t probe_cap(const grt_scene* s) {
+  const double c = 1.3 * s->desc.max_radius;
+  return c >= (double)PROBE_CAP ? PROBE_CAP : (c <= 4096.0 ? 4096u : (uint32_t)c);
+}
+
 // Probe-ordered tile queue (schedule.hip): worth its ~1/64 extra rays when a ray may run
 // far longer than an escaping one (max_steps well above the probe cap) over many tiles,
 // in the affine-parameter charts.  KerrBL integrates in Mino time, where even captured
@@ -403,7 +413,7 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   uint32_t* idx = (uint32_t*)take(n * 4);
   uint32_t* ord = (uint32_t*)take(n * 4);
   void* temp = take(temp_bytes);
-  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, PROBE_CAP, probe, stream));
+  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, probe_cap(s), probe, stream));
   HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, keys, keys_sorted, idx, ord, temp, &temp_bytes, stream));
   *order = ord;
   return 0;
