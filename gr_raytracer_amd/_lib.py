@@ -183,6 +183,8 @@ def lib() -> C.CDLL:
                                        C.POINTER(C.c_uint8), C.POINTER(AuxOut), C.POINTER(Stats)]),
         "grt_render_shard_async": (C.c_int, [vp, C.c_int, vp, C.POINTER(RowShard), vp, vp, vp, vp, vp, vp, vp]),
         "grt_adaptive_min_luminance": (_d, [_pd, u64, C.POINTER(AdaptiveConfig)]),
+        "grt_adaptive_min_luminance_device": (C.c_int, [C.c_int, vp, vp, u32, u64, C.POINTER(AdaptiveConfig),
+                                                        C.POINTER(_d)]),
         "grt_supersample_shard": (C.c_int, [vp, C.c_int, vp, C.POINTER(RowShard), C.POINTER(AdaptiveConfig), _d, vp, vp,
                                             _pd, vp, C.POINTER(C.c_uint64), vp]),
         "grt_write_png_rgb": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), u32, u32]),
@@ -220,7 +222,7 @@ EXPORTED_SYMBOLS = [
     "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config", "grt_set_schedule",
     "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",
-    "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_supersample_shard",
+    "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_adaptive_min_luminance_device", "grt_supersample_shard",
     "grt_write_png_rgb", "grt_write_hdr_xyz",
 ]
 

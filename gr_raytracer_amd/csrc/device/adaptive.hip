@@ -11,7 +11,10 @@
 //  * average_kernel: the ordered sum of the valid sub-samples and the 1/valid scale
 //    (supersample :334-380).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
+
+#include <cstring>
 
 #include "grt_api.h"
 #include "kernels.h"
@@ -144,7 +147,48 @@ __global__ void paint_kernel(const uint32_t* __restrict__ sel, uint64_t n_sel, d
   o[3] = m3;
 }
 
+// resolve_minimum_luminance's order (raytracer.rs:118-129): f64::total_cmp of the
+// luminance Y, as an unsigned radix key (total_cmp's signed key with the sign bit
+// flipped).  The map is its own inverse on the low 63 bits, so the selected key gives
+// back the exact f64.
+__device__ __forceinline__ uint64_t total_cmp_ukey(double v) {
+  const int64_t b = __double_as_longlong(v);
+  return (uint64_t)(b ^ (int64_t)((uint64_t)(b >> 63) >> 1)) ^ 0x8000000000000000ull;
+}
+
+__global__ void lum_keys_kernel(const double* __restrict__ y, uint32_t stride, uint64_t n,
+                                uint64_t* __restrict__ keys) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keys[i] = total_cmp_ukey(y[(uint64_t)stride * i]);
+}
+
 static inline unsigned nblocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t luminance_order_stat(const double* d_y, uint32_t stride, uint64_t n, uint64_t index, void* d_mem,
+                                size_t* mem_bytes, double* value, hipStream_t stream) {
+  size_t temp = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortKeys(nullptr, temp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                   (int)n, 0, 64, stream);
+  if (e != hipSuccess) return e;
+  const size_t keys_bytes = ((n * 8 + 255) & ~(size_t)255);
+  if (d_mem == nullptr) {
+    *mem_bytes = 2 * keys_bytes + temp;
+    return hipSuccess;
+  }
+  uint64_t* keys = (uint64_t*)d_mem;
+  uint64_t* sorted = (uint64_t*)((char*)d_mem + keys_bytes);
+  void* tmp = (char*)d_mem + 2 * keys_bytes;
+  hipLaunchKernelGGL(lum_keys_kernel, dim3(nblocks(n, 256)), dim3(256), 0, stream, d_y, stride, n, keys);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipcub::DeviceRadixSort::SortKeys(tmp, temp, keys, sorted, (int)n, 0, 64, stream)) != hipSuccess) return e;
+  uint64_t k = 0;
+  if ((e = hipMemcpyAsync(&k, sorted + index, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+  const int64_t sk = (int64_t)(k ^ 0x8000000000000000ull);
+  const int64_t b = sk ^ (int64_t)((uint64_t)(sk >> 63) >> 1);
+  std::memcpy(value, &b, 8);
+  return hipSuccess;
+}
 
 hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const AdaptiveParams& p,
                          uint8_t* d_flags, hipStream_t stream) {

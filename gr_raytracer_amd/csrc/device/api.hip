@@ -742,6 +742,37 @@ static double relative_min_luminance(std::vector<double>& lum) {
   return 1e-3 * lum[index];
 }
 
+// relative_min_luminance of n device luminances d_y[stride * i], selected on the device
+// (radix sort in f64::total_cmp order): the same element, without the host copy.
+static int device_relative_min_luminance(const double* d_y, uint32_t stride, uint64_t n, hipStream_t st,
+                                         double* out) {
+  if (n == 0) {
+    *out = 0.0;
+    return 0;
+  }
+  const uint64_t index = (uint64_t)((double)(n - 1) * 0.99);
+  size_t bytes = 0;
+  HIP_TRY(grt::luminance_order_stat(d_y, stride, n, index, nullptr, &bytes, nullptr, st));
+  DevBuf b_sort;
+  int rc = b_sort.alloc(bytes);
+  if (rc) return rc;
+  double v = 0.0;
+  HIP_TRY(grt::luminance_order_stat(d_y, stride, n, index, b_sort.p, &bytes, &v, st));
+  *out = 1e-3 * v;
+  return 0;
+}
+
+int grt_adaptive_min_luminance_device(int device, void* stream, const double* d_y, uint32_t stride, uint64_t n,
+                                      const grt_adaptive_config* cfg, double* out) {
+  if (!out || (n && (!d_y || stride == 0))) return fail(-EINVAL, "null argument");
+  if (cfg && cfg->has_minimum_luminance) {
+    *out = cfg->minimum_luminance;
+    return 0;
+  }
+  HIP_TRY(hipSetDevice(device));
+  return device_relative_min_luminance(d_y, stride, n, (hipStream_t)stream, out);
+}
+
 double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adaptive_config* cfg) {
   if (cfg && cfg->has_minimum_luminance) return cfg->minimum_luminance;
   if (!lum || n == 0) return 0.0;
@@ -784,12 +815,9 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
     // resolve_minimum_luminance (raytracer.rs:118-129): exact 99th percentile in
     // f64::total_cmp order, selected on the host from the device 1-spp buffer.
     double min_lum = cfg->minimum_luminance;
-    if (!cfg->has_minimum_luminance) {
-      std::vector<double> x64(4 * n), lum(n);
-      HIP_TRY(hipMemcpy(x64.data(), b_x64.p, n * 32, hipMemcpyDeviceToHost));
-      for (uint64_t i = 0; i < n; ++i) lum[i] = x64[4 * i + 1];
-      min_lum = relative_min_luminance(lum);
-    }
+    if (!cfg->has_minimum_luminance &&
+        (rc = device_relative_min_luminance((const double*)b_x64.p + 1, 4, n, st, &min_lum)))
+      return rc;
     grt::AdaptiveParams ap;
     ap.w = w;
     ap.h = h;

@@ -49,6 +49,10 @@ struct AdaptiveParams {
 };
 hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const AdaptiveParams& p,
                          uint8_t* d_flags, hipStream_t stream);
+// The index-th of n luminances d_y[stride * i] in f64::total_cmp order, on the device
+// (radix sort).  Call with d_mem == NULL for the scratch size.
+hipError_t luminance_order_stat(const double* d_y, uint32_t stride, uint64_t n, uint64_t index, void* d_mem,
+                                size_t* mem_bytes, double* value, hipStream_t stream);
 hipError_t launch_select_shard(const double* d_ya, const uint8_t* d_cls, const AdaptiveParams& p, uint32_t band_rows,
                                uint32_t shard, uint32_t n_shards, uint32_t local_rows, uint8_t* d_flags,
                                hipStream_t stream);

@@ -302,11 +302,12 @@ def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int
         if cfg.enabled or sampling_mask_xyza is not None:
             frame = allgather_frame(pack_luminance_records(xyza64, cls), rows, cols, band_rows, rank, world, group)
             frame_ya, frame_cls = unpack_luminance_records(frame)
-            if cfg.has_minimum_luminance:
-                min_lum = cfg.minimum_luminance
-            else:
-                lum = np.ascontiguousarray(frame_ya[:, 0].cpu().numpy())
-                min_lum = lib.grt_adaptive_min_luminance(L.dptr(lum), lum.shape[0], C.byref(cfg))
+            # the frame's exact 99th-percentile floor, selected on this GPU (no host copy)
+            floor = C.c_double(0.0)
+            L.check(lib.grt_adaptive_min_luminance_device(device, stream.cuda_stream, frame_ya.data_ptr(), 2,
+                                                          frame_ya.shape[0], C.byref(cfg), C.byref(floor)),
+                    "grt_adaptive_min_luminance_device")
+            min_lum = floor.value
             mask = None
             if sampling_mask_xyza is not None:
                 mask = (C.c_double * 4)(*[float(v) for v in sampling_mask_xyza])

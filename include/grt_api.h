@@ -406,6 +406,10 @@ int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt
 /* resolve_minimum_luminance (raytracer.rs:118-129): cfg->minimum_luminance when set,
  * else 1e-3 x the ((n-1) * 0.99)-th luminance in f64::total_cmp order (0 when n = 0). */
 double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adaptive_config* cfg);
+/* The same value from n DEVICE luminances d_y[stride * i] on `device`, selected on the
+ * GPU (radix sort in total_cmp order; synchronises `stream`).  Returns 0 or -errno. */
+int grt_adaptive_min_luminance_device(int device, void* stream, const double* d_y, uint32_t stride, uint64_t n,
+                                      const grt_adaptive_config* cfg, double* out);
 
 /* collect_pixels_to_supersample (raytracer.rs:386-458) over the local pixels of shard
  * `sh` + supersample (:320-384), on `device`, enqueued on `stream` and synchronised

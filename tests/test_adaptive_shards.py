@@ -259,3 +259,32 @@ def test_grt_cli_logs_failed_pixels_like_the_reference(grt, oracle, gpu, tmp_pat
     st = ref["status"].reshape(64, 64) & 0x7F
     want = {(int(c), int(rw), names[int(st[rw, c])]) for rw, c in zip(*np.nonzero(st))}
     assert len(want) > 10 and got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 101, 4097, 250001])
+def test_device_floor_equals_host_floor(grt, gpu, n):
+    """grt_adaptive_min_luminance_device (radix sort on the GPU) selects the same f64 as
+    the host's nth_element in total_cmp order, special values included."""
+    import torch
+
+    from gr_raytracer_amd import _lib as L
+
+    rng = np.random.default_rng(n)
+    lum = rng.exponential(size=n) * rng.choice([1e-9, 1.0, 1e3], size=n)
+    if n > 10:
+        lum[:6] = [0.0, -0.0, np.inf, -np.inf, np.nan, -np.nan]
+        rng.shuffle(lum)
+    cfg = L.AdaptiveConfig()
+    L.lib().grt_default_adaptive_config(C.byref(cfg))
+    cfg.has_minimum_luminance = 0
+    want = L.lib().grt_adaptive_min_luminance(L.dptr(np.ascontiguousarray(lum)), n, C.byref(cfg))
+    for stride in (1, 2, 4):
+        a = np.zeros(n * stride)
+        a[::stride] = lum
+        d = torch.from_numpy(a).to(torch.device("cuda", 0))
+        got = C.c_double()
+        L.check(L.lib().grt_adaptive_min_luminance_device(0, None, d.data_ptr(), stride, n, C.byref(cfg),
+                                                          C.byref(got)), "grt_adaptive_min_luminance_device")
+        assert struct.pack("<d", got.value) == struct.pack("<d", want) or (np.isnan(got.value) and np.isnan(want))
+
