@@ -1,6 +1,6 @@
 """bench.py — geodesic steps/sec/GPU on the reference's C2 configuration.
 
-Workload (BASELINE.json configs[1]): 1500x1500 scene-definitions/schwarzschild.toml,
+Default workload (BASELINE.json configs[1]): 1500x1500 scene-definitions/schwarzschild.toml,
 --max-steps=1e5, camera from README.md:63 (--camera-position=-16,0,3.5 --theta=-3.142),
 1 sample per pixel (adaptive sampling off).  One bench "step" = one full 1500x1500
 frame traced on the GPU (every pixel integrated to its stop condition, every window
@@ -11,9 +11,16 @@ scaling over a batch of frames: rank r renders frame r of a camera fly-by (the c
 orbits the hole by r * 1e-3 rad), then the f32 frames are gathered to rank 0 over RCCL.
 value = accepted steps of all ranks / max-over-ranks wall time.
 
+--workload c4 (BASELINE.json configs[3], the north-star layout): ONE 4096x4096 kerr.toml
+frame (Kerr-Schild, max-steps 1e6, camera of docs/example-render-commands.md:29-37)
+row-tiled across the N ranks (cyclic 16-row bands, grt_render_shard_async) and gathered
+to rank 0 in one RCCL gather (gr_raytracer_amd.distributed.gather_frame).  Strong
+scaling; the line carries each rank's kernel time, the max/mean imbalance and the
+gather time.  A 4096^2 frame takes minutes per GPU: run it with --steps 1 --warmup 0.
+
 Printed JSON carries the FP64 VALU roofline of the trace kernel (HIP events on the launch
 stream) and the CPU baseline: the oracle (reference algorithm restated in C++, stored
-trajectories + post-hoc window pass) timed on the host cores on a bounded row sample.
+trajectories + post-hoc window pass) timed on the host cores on a bounded sample.
 """
 from __future__ import annotations
 
@@ -28,15 +35,22 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+METRIC = "geodesic steps/sec/GPU + wall-clock for 1500x1500 Schwarzschild render"
 # algorithmic FP64 flops per accepted step = F_att * n_att + F_step
 FLOPS = {  # geometry: (flops per RKF45 attempt, extra flops per accepted step)
     "schwarzschild": (733.0, 50.0),
     "kerr_bl": (865.0, 38.0),
     "kerr": (9913.0, 67.0),
 }
-FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (AMD spec); see DESIGN.md
-HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip table
+FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (AMD spec, FMA = 2 flops); see DESIGN.md
+FP64_MEASURED_PEAK_TFLOPS = 61.8  # tools/fp64_peak.hip, profiles/r01/fp64_peak.json
+# the path is compiled without contraction: every flop is one add / mul / div instruction
+# slot, so the issue ceiling for this arithmetic is half the FMA peak
+FP64_NO_CONTRACTION_TFLOPS = FP64_VECTOR_PEAK_TFLOPS / 2
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table
 BYTES_PER_PIXEL_OUT = 16 + 1 + 1  # f32 XYZA + class + status
+PMC_FILE = {"c2": ROOT / "profiles" / "r02_c2_pmc.json", "c4": ROOT / "profiles" / "r02_c4_pmc.json"}
+SCENES = ROOT / "tests" / "golden" / "scenes"
 
 
 def c2_opts(g, frame: int = 0):
@@ -47,67 +61,146 @@ def c2_opts(g, frame: int = 0):
                         max_steps=100000)
 
 
-def cpu_baseline(g, seconds_budget: float = 20.0) -> dict:
-    """Oracle (reference algorithm) on rows = 0 mod 64 of the C2 frame, host cores."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import pyoracle as O  # noqa: E402  (test infrastructure: the checker/baseline only)
+def c4_opts(g, size: int = 4096, max_steps: int = 1000000):
+    return g.GlobalOpts(width=size, height=size, camera_position=(-10.0, 0.0, -0.5), theta=1.52, psi=-1.57,
+                        phi=0.0, max_steps=max_steps)
 
+
+# ----------------------------------------------------------------- host cores ----
+def host_cores() -> dict:
+    """The CPUs this process may use: its affinity set, the cgroup CPU quota (the GPU
+    box's lease), physical cores and SMT among them."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = sorted(os.sched_getaffinity(0))
     except Exception:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16
-    hs = g.HostScene(str(ROOT / "tests/golden/scenes/schwarzschild.toml"), c2_opts(g),
-                     str(ROOT / "tests/golden"))
-    rows = list(range(0, 1500, 64))
-    t0 = time.time()
-    r = O.render_pixels(hs.desc, 0, 0, 1500, 1500, threads=cores, row_list=rows)
-    wall = time.time() - t0
+        aff = list(range(os.cpu_count() or 1))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = float(q) / float(period)
+    except Exception:
+        pass
+    phys = set()
     model = ""
     try:
-        with open("/proc/cpuinfo") as f:
-            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
-    except OSError:
+        cpu = core = pkg = None
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("processor"):
+                cpu = int(ln.split(":")[1])
+            elif ln.startswith("physical id"):
+                pkg = ln.split(":")[1].strip()
+            elif ln.startswith("core id"):
+                core = ln.split(":")[1].strip()
+            elif ln.startswith("model name") and not model:
+                model = ln.split(":", 1)[1].strip()
+            elif not ln.strip() and cpu is not None:
+                if cpu in aff:
+                    phys.add((pkg, core))
+                cpu = core = pkg = None
+    except Exception:
         pass
-    return {"value": r["accepted"] / r["wall_s"], "unit": "geodesic steps/s", "cores": cores, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(),
-            "full_frame_s_extrapolated": round(r["wall_s"] * 1500 / len(rows), 1),
-            "sample": f"C2 frame rows 0 mod 64 ({len(rows)} rows x 1500 px = {len(rows) * 1500} rays, "
-                      f"{r['accepted']} accepted steps in {r['wall_s']:.1f} s, OpenMP dynamic over pixels)",
-            "wall_s": round(wall, 2)}
+    smt = None
+    try:
+        smt = Path("/sys/devices/system/cpu/smt/active").read_text().strip() == "1"
+    except Exception:
+        pass
+    threads = len(aff)
+    if quota is not None:  # more runnable threads than the quota only adds throttling
+        threads = max(1, min(threads, int(math.ceil(quota))))
+    return {"threads": threads, "affinity_cpus": len(aff), "cgroup_cpu_quota": quota,
+            "physical_cores_in_affinity": len(phys) or None, "smt_active": smt, "cpu_model": model,
+            "host_cpus": os.cpu_count()}
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--blocks-per-cu", type=int, default=0)
-    args = ap.parse_args()
+def cpu_baseline(g, workload: str = "c2") -> dict:
+    """The oracle (reference algorithm, kind "port") on a bounded sample of the same
+    workload, on every host core this process may use (affinity set, capped only by the
+    cgroup quota when one is set)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    import pyoracle as O  # noqa: E402  (test infrastructure: the checker/baseline only)
 
+    hc = host_cores()
+    cores = hc["threads"]
+    if workload == "c4":
+        hs = g.HostScene(str(SCENES / "kerr.toml"), c4_opts(g), str(ROOT / "tests/golden"))
+        rng = np.random.default_rng(13)
+        cell = 128
+        r0, c0 = np.meshgrid(np.arange(0, 4096, cell), np.arange(0, 4096, cell), indexing="ij")
+        ri = (r0.ravel() + rng.random(r0.size) * cell).astype(np.int64)
+        ci = (c0.ravel() + rng.random(c0.size) * cell).astype(np.int64)
+        pix = (ri * 4096 + ci).astype(np.uint32)
+        half = np.full(pix.size, 0.5)
+        t0 = time.time()
+        r = O.render_pixels(hs.desc, 0, 0, 4096, 4096, threads=cores, offsets=(pix, half, half))
+        wall = time.time() - t0
+        sample = (f"C4 frame, 1024 stratified pixels (one per 128x128 cell, pixel centre), {r['accepted']} accepted "
+                  f"steps in {r['wall_s']:.1f} s, OpenMP dynamic over pixels")
+        extra = {}
+    else:
+        hs = g.HostScene(str(SCENES / "schwarzschild.toml"), c2_opts(g), str(ROOT / "tests/golden"))
+        stride = 16 if cores >= 64 else 64  # SURVEY 8(d): rows = 0 mod 16 on a large host
+        rows = list(range(0, 1500, stride))
+        t0 = time.time()
+        r = O.render_pixels(hs.desc, 0, 0, 1500, 1500, threads=cores, row_list=rows)
+        wall = time.time() - t0
+        sample = (f"C2 frame rows 0 mod {stride} ({len(rows)} rows x 1500 px = {len(rows) * 1500} rays, "
+                  f"{r['accepted']} accepted steps in {r['wall_s']:.1f} s, OpenMP dynamic over pixels)")
+        extra = {"full_frame_s_extrapolated": round(r["wall_s"] * 1500 / len(rows), 1)}
+    out = {"value": r["accepted"] / r["wall_s"], "unit": "geodesic steps/s", "cores": cores, "kind": "port",
+           "sample": sample, "wall_s": round(wall, 2)}
+    out.update(extra)
+    out.update({k: v for k, v in hc.items() if k != "threads"})
+    return out
+
+
+# ------------------------------------------------------------------- roofline ----
+def roofline(workload: str, geometry: str, accepted: float, attempts: float, kernel_ms: float,
+             n_pixels: int, kernel_name: str) -> dict:
+    """FP64 VALU roofline of the integrate kernel for one launch (counts per launch)."""
+    from gr_raytracer_amd import _lib as L
+
+    f_att, f_step = FLOPS[geometry]
+    flop = f_att * attempts + f_step * accepted
+    achieved = flop / (kernel_ms * 1e-3) / 1e12
+    out = {"bound": "valu-fp64", "achieved": achieved, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
+           "frac_measured_peak": achieved / FP64_MEASURED_PEAK_TFLOPS,
+           "frac_no_contraction": achieved / FP64_NO_CONTRACTION_TFLOPS,
+           "traffic": None, "kernel": kernel_name, "kernel_ms": kernel_ms, "flop_per_launch": flop,
+           "flop_model": f"{f_att:g}*attempts + {f_step:g}*accepted (SURVEY 8d)",
+           "hbm_algorithmic_GBps": n_pixels * BYTES_PER_PIXEL_OUT / (kernel_ms * 1e-3) / 1e9,
+           "hbm_peak_GBps": HBM_PEAK_GBS}
+    prof = PMC_FILE.get(workload)
+    if prof is not None and prof.exists():
+        pmc = json.loads(prof.read_text())
+        mine = L.device_code_sha256()
+        if pmc.get("code_object_sha256") != mine:
+            out["traffic_note"] = f"{prof.name} was taken from another build of the device code: not used"
+        else:
+            out["traffic"] = pmc.get("hbm_bytes_per_launch")
+            out["pmc_file"] = os.path.relpath(prof, ROOT)
+            for k in ("active_valu_over_wave_cycles", "lane_utilisation", "valu_f64_fraction",
+                      "wait_inst_any_over_wave_cycles", "scratch_bytes_per_launch"):
+                if k in pmc:
+                    out[k] = pmc[k]
+    else:
+        out["traffic_note"] = "no PMC summary for this workload"
+    return out
+
+
+# ------------------------------------------------------------------ workloads ----
+def run_c2(args, rank, world, local_rank, dev):
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    else:
-        torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
 
     import gr_raytracer_amd as g
     from gr_raytracer_amd import _lib as L
 
     lib = L.lib()
-    if args.blocks_per_cu:
-        L.check(lib.grt_set_launch_config(args.blocks_per_cu, 256), "grt_set_launch_config")
     opts = c2_opts(g, frame=rank)
-    hs = g.HostScene(str(ROOT / "tests/golden/scenes/schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
+    hs = g.HostScene(str(SCENES / "schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
     scene = g.Scene(hs.desc_ptr(), keepalive=hs)
     rows, cols = opts.height, opts.width
     n = rows * cols
@@ -156,52 +249,200 @@ def main() -> None:
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
     total_acc, total_att = float(t[1]), float(t[2])
+    if rank != 0:
+        return None
+    line = {
+        "metric": METRIC,
+        "value": total_acc / elapsed,
+        "unit": "accepted RKF45 geodesic steps/s (whole job)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: reference scene schwarzschild.toml + its textures (vendored fixtures)",
+        "config": {"workload": "C2: 1500x1500 schwarzschild.toml, max-steps=1e5, camera -16,0,3.5 "
+                               "theta=-3.142, 1 spp (adaptive off); one step = one frame per GPU",
+                   "frame_pixels": n, "parallelism": f"frames x{world} (one frame per GPU), RCCL gather",
+                   "steps_per_gpu_per_s": total_acc / elapsed / world,
+                   "attempts_per_accepted": total_att / max(total_acc, 1.0),
+                   "frame_wall_s_per_gpu": elapsed / args.steps},
+        "roofline": roofline("c2", "schwarzschild", accepted / args.steps, attempts / args.steps, kernel_ms, n,
+                             "grt::integrate_kernel<1, false> (Schwarzschild; events also span shade_kernel<1, 0>, "
+                             "<0.01%)"),
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(g, "c2")
+    return line
 
-    if rank == 0:
-        f_att, f_step = FLOPS["schwarzschild"]
-        acc_per_launch = accepted / args.steps
-        att_per_launch = attempts / args.steps
-        flop_per_launch = f_att * att_per_launch + f_step * acc_per_launch
-        achieved_tflops = flop_per_launch / (kernel_ms * 1e-3) / 1e12
-        prof = ROOT / "profiles" / "r01t_pmc.json"  # PMC passes of this kernel, tools/run_pmc.sh
-        traffic = None
-        if prof.exists():
-            try:
-                traffic = json.loads(prof.read_text()).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        line = {
-            "metric": "geodesic steps/sec/GPU + wall-clock for 1500x1500 Schwarzschild render",
-            "value": total_acc / elapsed,
-            "unit": "accepted RKF45 geodesic steps/s (whole job)",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: reference scene schwarzschild.toml + its textures (vendored fixtures)",
-            "config": {"workload": "C2: 1500x1500 schwarzschild.toml, max-steps=1e5, camera -16,0,3.5 "
-                                   "theta=-3.142, 1 spp (adaptive off); one step = one frame per GPU",
-                       "frame_pixels": n, "parallelism": f"frames x{world} (one frame per GPU), RCCL gather",
-                       "steps_per_gpu_per_s": total_acc / elapsed / world,
-                       "attempts_per_accepted": total_att / max(total_acc, 1.0),
-                       "frame_wall_s_per_gpu": elapsed / args.steps},
-            "roofline": {"bound": "valu-fp64", "achieved": achieved_tflops, "peak": FP64_VECTOR_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tflops / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": traffic, "kernel": "grt::integrate_kernel<1, false> (Schwarzschild; events also span shade_kernel<1, 0>, <0.01%)",
-                         "kernel_ms": kernel_ms, "flop_per_launch": flop_per_launch,
-                         "flop_model": f"{f_att:g}*attempts + {f_step:g}*accepted (SURVEY 8d)",
-                         "hbm_algorithmic_GBps": n * BYTES_PER_PIXEL_OUT / (kernel_ms * 1e-3) / 1e9,
-                         "hbm_peak_GBps": HBM_PEAK_GBS},
-            "cpu_baseline": None,
-        }
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(g)
-        print(json.dumps(line), flush=True)
+
+def c4_frame_steps(trace_shard, rank: int, world: int, frame_rows: int, cols: int, band_rows: int,
+                   steps: int, warmup: int, sync, group=None):
+    """The C4 strong-scaling loop, backend-agnostic (RCCL on the GPUs, gloo in tests).
+
+    trace_shard() traces this rank's row bands and returns (records (n_local, 18) u8,
+    accepted, attempts, kernel_ms); sync() waits for the rank's device.  Per step:
+    barrier, trace, barrier (every rank's kernel done), ONE gather of the records to
+    rank 0.  Returns this rank's per-step lists and the frames' accepted/attempt sums."""
+    import torch.distributed as dist
+
+    from gr_raytracer_amd.distributed import gather_frame
+
+    for _ in range(warmup):
+        rec, _, _, _ = trace_shard()
+        gather_frame(rec, frame_rows, cols, band_rows, rank, world, 0, group)
+    sync()
+    kernel_ms, gather_ms, step_s = [], [], []
+    acc = att = 0.0
+    frame = None
+    for _ in range(steps):
+        dist.barrier(group=group)
+        sync()
+        t0 = time.perf_counter()
+        rec, a, b, kms = trace_shard()
+        sync()
+        acc += a
+        att += b
+        kernel_ms.append(kms)
+        dist.barrier(group=group)  # every rank's shard is traced
+        t1 = time.perf_counter()
+        frame = gather_frame(rec, frame_rows, cols, band_rows, rank, world, 0, group)
+        sync()
+        t2 = time.perf_counter()
+        gather_ms.append((t2 - t1) * 1e3)
+        step_s.append(t2 - t0)
+    return {"kernel_ms": kernel_ms, "gather_ms": gather_ms, "step_s": step_s, "accepted": acc, "attempts": att,
+            "frame": frame}
+
+
+def c4_summary(res: dict, rank: int, world: int, device="cpu", group=None) -> dict:
+    """Reduce c4_frame_steps' per-rank results: max-over-ranks step time, per-rank
+    kernel ms, imbalance = max / mean kernel ms, gather ms on rank 0."""
+    import torch
+    import torch.distributed as dist
+
+    steps = len(res["step_s"])
+    mine = torch.tensor([sum(res["step_s"]), sum(res["kernel_ms"]) / steps, res["accepted"], res["attempts"]],
+                        dtype=torch.float64, device=device)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine, group=group)
+    allv = [v.cpu() for v in allv]
+    if rank != 0:
+        return None
+    per_rank_ms = [float(v[1]) for v in allv]
+    elapsed = max(float(v[0]) for v in allv)
+    mean_ms = sum(per_rank_ms) / world
+    return {"elapsed_s": elapsed, "per_rank_kernel_ms": per_rank_ms,
+            "imbalance": max(per_rank_ms) / mean_ms if mean_ms > 0 else 1.0,
+            "gather_ms": sum(res["gather_ms"]) / steps,
+            "accepted": sum(float(v[2]) for v in allv), "attempts": sum(float(v[3]) for v in allv),
+            "rank0_accepted": float(allv[0][2]), "rank0_attempts": float(allv[0][3]), "steps": steps}
+
+
+def run_c4(args, rank, world, local_rank, dev):
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    import gr_raytracer_amd as g
+    from gr_raytracer_amd import _lib as L
+    from gr_raytracer_amd.distributed import pack_records, shard_row_count
+
+    lib = L.lib()
+    opts = c4_opts(g, args.size)
+    hs = g.HostScene(str(SCENES / "kerr.toml"), opts, str(ROOT / "tests/golden"))
+    scene = g.Scene(hs.desc_ptr(), keepalive=hs)
+    rows, cols, band = opts.height, opts.width, args.band_rows
+    n_local = shard_row_count(rows, band, rank, world) * cols
+    xyza = torch.empty((n_local, 4), dtype=torch.float32, device=dev)
+    cls = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    status = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = L.RowShard(band, rank, world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def trace_shard():
+        stats.zero_()
+        e0.record(stream)
+        L.check(lib.grt_render_shard_async(scene._s, local_rank, stream.cuda_stream, C.byref(sh), xyza.data_ptr(),
+                                           cls.data_ptr(), status.data_ptr(), None, None, None, stats.data_ptr()),
+                "grt_render_shard_async")
+        e1.record(stream)
+        e1.synchronize()
+        c = stats.cpu().tolist()
+        return pack_records(xyza, cls, status), float(c[0]), float(c[1]), e0.elapsed_time(e1)
+
+    res = c4_frame_steps(trace_shard, rank, world, rows, cols, band, args.steps, args.warmup,
+                         lambda: torch.cuda.synchronize(dev))
+    s = c4_summary(res, rank, world, dev)
+    if rank != 0:
+        return None
+    line = {
+        "metric": METRIC,
+        "value": s["accepted"] / s["elapsed_s"],
+        "unit": "accepted RKF45 geodesic steps/s (whole job)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": s["elapsed_s"] / s["steps"] * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: reference scene kerr.toml + its textures (vendored fixtures)",
+        "config": {"workload": f"C4: {cols}x{rows} kerr.toml (Kerr-Schild), max-steps=1e6, camera -10,0,-0.5 "
+                               "theta=1.52 psi=-1.57, 1 spp; one step = one frame row-tiled across the ranks",
+                   "frame_pixels": rows * cols, "band_rows": band,
+                   "parallelism": f"cyclic {band}-row bands x{world}, one RCCL gather to rank 0",
+                   "steps_per_gpu_per_s": s["accepted"] / s["elapsed_s"] / world,
+                   "attempts_per_accepted": s["attempts"] / max(s["accepted"], 1.0),
+                   "frame_wall_s": s["elapsed_s"] / s["steps"]},
+        "per_rank_kernel_ms": s["per_rank_kernel_ms"],
+        "imbalance": s["imbalance"],
+        "gather_ms": s["gather_ms"],
+        "gather_GBps": rows * cols * BYTES_PER_PIXEL_OUT / (s["gather_ms"] * 1e-3) / 1e9 if s["gather_ms"] else None,
+        "roofline": roofline("c4", "kerr", s["rank0_accepted"] / s["steps"], s["rank0_attempts"] / s["steps"],
+                             s["per_rank_kernel_ms"][0], n_local, "grt::integrate_kernel<2, false> (Kerr-Schild; "
+                             "events also span the probe pass and shade_kernel<2, 0>), rank 0's shard"),
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(g, "c4")
+    return line
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=("c2", "c4"), default="c2")
+    ap.add_argument("--size", type=int, default=4096, help="c4: frame edge (4096 = configs[3])")
+    ap.add_argument("--band-rows", type=int, default=16, help="c4: rows per cyclic band")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--blocks-per-cu", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
     if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    elif args.workload == "c4":  # the c4 loop uses barriers: a group of one
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+
+    from gr_raytracer_amd import _lib as L
+
+    if args.blocks_per_cu:
+        L.check(L.lib().grt_set_launch_config(args.blocks_per_cu, 256), "grt_set_launch_config")
+    line = (run_c4 if args.workload == "c4" else run_c2)(args, rank, world, local_rank, dev)
+    if line is not None:
+        print(json.dumps(line), flush=True)
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

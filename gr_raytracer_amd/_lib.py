@@ -239,3 +239,29 @@ def dptr(arr) -> _pd:
 
 def ptr(arr, ctype):
     return arr.ctypes.data_as(C.POINTER(ctype))
+
+
+def device_code_sha256(path: Path = LIB_PATH) -> str:
+    """SHA-256 of the gfx950 device code inside libgrt.so (its ELF `.hip_fatbin`
+    section: every kernel's code object).  PMC summaries under profiles/ record it, and
+    bench.py refuses a summary taken from another build."""
+    import hashlib
+    import struct
+
+    data = Path(path).read_bytes()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise GrtError(f"{path}: not an ELF64 file")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def section(i):
+        name, _type, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+
+    _, str_off, _ = section(shstrndx)
+    for i in range(shnum):
+        name, off, size = section(i)
+        end = data.index(b"\0", str_off + name)
+        if data[str_off + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()
+    raise GrtError(f"{path}: no .hip_fatbin section")

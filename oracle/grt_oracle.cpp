@@ -1746,6 +1746,40 @@ static int total_cmp(double a, double b) {  // f64::total_cmp
   return ia < ib ? -1 : (ia > ib ? 1 : 0);
 }
 
+// resolve_minimum_luminance (raytracer.rs:118-129) + collect_pixels_to_supersample
+// (:386-458) over a w x h section buffer (row-major): the serial stencil, first trigger
+// wins.  Returns the luminance floor; `sel` gets the selected section indices in order.
+static double select_pixels(const std::vector<Sample>& buf, uint32_t w, uint32_t hgt,
+                            const grt_adaptive_config& cfg, std::vector<uint64_t>* sel) {
+  const uint64_t n = (uint64_t)w * hgt;
+  double min_lum;
+  if (cfg.has_minimum_luminance) min_lum = cfg.minimum_luminance;
+  else if (n == 0) min_lum = 0.0;
+  else {
+    std::vector<double> lum(n);
+    for (uint64_t i = 0; i < n; ++i) lum[i] = buf[i].color.y;
+    uint64_t index = (uint64_t)((double)(n - 1) * 0.99);
+    std::nth_element(lum.begin(), lum.begin() + index, lum.end(),
+                     [](double a, double b) { return total_cmp(a, b) < 0; });
+    min_lum = 1e-3 * lum[index];
+  }
+  static const int shifts[8][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 1}, {1, -1}, {1, 0}, {1, 1}};
+  for (uint32_t row = 0; row < hgt; ++row)
+    for (uint32_t col = 0; col < w; ++col) {
+      uint64_t pi = (uint64_t)row * w + col;
+      for (int s = 0; s < 8; ++s) {
+        int64_t nr = (int64_t)row + shifts[s][0], nc = (int64_t)col + shifts[s][1];
+        if (nr < 0 || nr >= (int64_t)hgt || nc < 0 || nc >= (int64_t)w) continue;
+        uint64_t ni = (uint64_t)nr * w + (uint64_t)nc;
+        if (should_supersample_pair(buf[pi], buf[ni], cfg, min_lum)) {
+          sel->push_back(pi);
+          break;
+        }
+      }
+    }
+  return min_lum;
+}
+
 }  // namespace oracle
 
 // =================================================================== C ABI =====
@@ -1850,31 +1884,8 @@ uint64_t oracle_render_section(const grt_scene_desc* d, uint32_t from_row, uint3
     if (cls_out) cls_out[i] = (uint8_t)buf[i].ray_class;
   }
   if (!supersampled) return 0;
-  // resolve_minimum_luminance :118-129
-  double min_lum;
-  if (cfg->has_minimum_luminance) min_lum = cfg->minimum_luminance;
-  else if (n == 0) min_lum = 0.0;
-  else {
-    std::vector<double> lum(n);
-    for (uint64_t i = 0; i < n; ++i) lum[i] = buf[i].color.y;
-    uint64_t index = (uint64_t)((double)(n - 1) * 0.99);
-    std::nth_element(lum.begin(), lum.begin() + index, lum.end(),
-                     [](double a, double b) { return total_cmp(a, b) < 0; });
-    min_lum = 1e-3 * lum[index];
-  }
-  // collect_pixels_to_supersample :386-458 (serial, first trigger wins)
-  static const int shifts[8][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 1}, {1, -1}, {1, 0}, {1, 1}};
   std::vector<uint64_t> sel;
-  for (uint32_t row = from_row; row < to_row; ++row)
-    for (uint32_t col = from_col; col < to_col; ++col) {
-      uint64_t pi = (uint64_t)(row - from_row) * w + (col - from_col);
-      for (int s = 0; s < 8; ++s) {
-        int nr = (int)row + shifts[s][0], nc = (int)col + shifts[s][1];
-        if (nr < (int)from_row || nr >= (int)to_row || nc < (int)from_col || nc >= (int)to_col) continue;
-        uint64_t ni = (uint64_t)(nr - (int)from_row) * w + (nc - (int)from_col);
-        if (should_supersample_pair(buf[pi], buf[ni], *cfg, min_lum)) { sel.push_back(pi); break; }
-      }
-    }
+  (void)select_pixels(buf, w, hgt, *cfg, &sel);
   if (mask_xyza) {
     for (uint64_t pi : sel) for (int k = 0; k < 4; ++k) out[4 * pi + k] = mask_xyza[k];
     return sel.size();
@@ -2195,6 +2206,22 @@ int oracle_should_supersample_pair(const double* p, int pc, const double* q, int
   b.color = XYZA{q[0], q[1], q[2], q[3]};
   b.ray_class = qc;
   return should_supersample_pair(a, b, *c, min_lum) ? 1 : 0;
+}
+// collect_pixels_to_supersample applied to a given 1-spp section buffer (f64 XYZA + class,
+// row-major w x h): flags_out[i] = 1 for the selected pixels.  Returns the luminance floor.
+double oracle_select_pixels(const double* xyza, const uint8_t* cls, uint32_t w, uint32_t h,
+                            const grt_adaptive_config* cfg, uint8_t* flags_out) {
+  const uint64_t n = (uint64_t)w * h;
+  std::vector<Sample> buf(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    buf[i].color = XYZA{xyza[4 * i], xyza[4 * i + 1], xyza[4 * i + 2], xyza[4 * i + 3]};
+    buf[i].ray_class = cls[i];
+  }
+  std::vector<uint64_t> sel;
+  double min_lum = select_pixels(buf, w, h, *cfg, &sel);
+  std::memset(flags_out, 0, n);
+  for (uint64_t pi : sel) flags_out[pi] = 1;
+  return min_lum;
 }
 }  // extern "C"
 

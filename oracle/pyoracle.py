@@ -40,6 +40,8 @@ def lib():
         L.oracle_render_section.restype = C.c_uint64
         L.oracle_render_section.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, _pd, _pd, _u8p,
                                             C.c_int]
+        L.oracle_select_pixels.restype = _d
+        L.oracle_select_pixels.argtypes = [_pd, _u8p, C.c_uint32, C.c_uint32, vp, _u8p]
         L.oracle_rk_analytic.argtypes = [_d, _pd, _pd]
         L.oracle_integrate_ray.restype = C.c_int64
         L.oracle_integrate_ray.argtypes = [vp, _pd, _pd, _pd, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -130,6 +132,18 @@ def render_section(desc, from_row, from_col, to_row, to_col, adaptive, mask=None
                                        C.cast(C.pointer(adaptive), C.c_void_p), _dp(m) if m is not None else None,
                                        _dp(out), cls.ctypes.data_as(_u8p), threads)
     return out, cls, int(nsel)
+
+
+def select_pixels(xyza, cls, w, h, adaptive):
+    """collect_pixels_to_supersample (raytracer.rs:386-458) + the luminance floor (:118-129)
+    applied to a given 1-spp section buffer: (bool flags (h*w,), min_luminance)."""
+    x = np.ascontiguousarray(xyza, np.float64).reshape(-1, 4)
+    c = np.ascontiguousarray(cls, np.uint8)
+    assert len(x) == len(c) == w * h
+    flags = np.zeros(w * h, np.uint8)
+    min_lum = lib().oracle_select_pixels(_dp(x), c.ctypes.data_as(_u8p), w, h,
+                                         C.cast(C.pointer(adaptive), C.c_void_p), flags.ctypes.data_as(_u8p))
+    return flags.astype(bool), float(min_lum)
 
 
 def rk_analytic(t_end):

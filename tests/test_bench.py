@@ -1,0 +1,126 @@
+"""bench.py's host logic on CPU: the C4 strong-scaling loop over gloo (world 2), the
+host-core census, and the roofline's refusal of a PMC summary from another build.
+
+The C4 loop (bench.c4_frame_steps / c4_summary) is backend-agnostic; here each rank's
+shard trace is the oracle (this container has no GPU), at a reduced frame size.  The
+gathered frame must equal a single-process oracle render, and the summary must carry
+the per-rank kernel times, the max/mean imbalance and the gather time.
+"""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, host_scene
+
+SIZE = 24
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _opts(g):
+    import bench
+
+    o = bench.c4_opts(g, SIZE, max_steps=3000)
+    o.max_radius = 100.0
+    return o
+
+
+def _worker(rank, world, port, band_rows, out_dir):
+    import sys
+    import time
+
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import gr_raytracer_amd as g
+    import pyoracle as O
+    from gr_raytracer_amd.distributed import pack_records, shard_frame_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hs = host_scene(g, "kerr.toml", _opts(g))
+        rows = shard_frame_rows(SIZE, band_rows, rank, world)
+
+        def trace_shard():
+            t0 = time.perf_counter()
+            r = O.render_pixels(hs.desc, 0, 0, SIZE, SIZE, threads=2, row_list=rows)
+            rec = pack_records(torch.from_numpy(r["xyza"].astype(np.float32)), torch.from_numpy(r["ray_class"]),
+                               torch.from_numpy(r["status"]))
+            return rec, float(r["accepted"]), float(r["attempts"]), (time.perf_counter() - t0) * 1e3
+
+        res = bench.c4_frame_steps(trace_shard, rank, world, SIZE, SIZE, band_rows, steps=2, warmup=1,
+                                   sync=lambda: None)
+        s = bench.c4_summary(res, rank, world)
+        if rank == 0:
+            frame = res["frame"].numpy()
+            np.save(os.path.join(out_dir, "frame.npy"), frame)
+            s = {k: v for k, v in s.items()}
+            with open(os.path.join(out_dir, "summary.json"), "w") as f:
+                json.dump(s, f)
+        else:
+            assert s is None and res["frame"] is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c4_strong_scaling_loop_gloo_world2(grt, oracle):
+    import torch.multiprocessing as mp
+
+    from gr_raytracer_amd.distributed import pack_records
+
+    import torch
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), 4, d), nprocs=2, join=True)
+        frame = np.load(os.path.join(d, "frame.npy"))
+        s = json.load(open(os.path.join(d, "summary.json")))
+    hs = host_scene(grt, "kerr.toml", _opts(grt))
+    ref = oracle.render_pixels(hs.desc, 0, 0, SIZE, SIZE, threads=4)
+    want = pack_records(torch.from_numpy(ref["xyza"].astype(np.float32)), torch.from_numpy(ref["ray_class"]),
+                        torch.from_numpy(ref["status"])).numpy()
+    assert np.array_equal(frame, want)
+    assert len(s["per_rank_kernel_ms"]) == 2 and all(v > 0 for v in s["per_rank_kernel_ms"])
+    assert s["imbalance"] >= 1.0
+    assert s["gather_ms"] > 0
+    assert s["steps"] == 2
+    assert s["accepted"] == 2 * ref["accepted"]  # two frames, every rank's steps
+
+
+def test_host_cores_census():
+    import bench
+
+    hc = bench.host_cores()
+    assert hc["threads"] >= 1
+    assert hc["affinity_cpus"] == len(os.sched_getaffinity(0))
+    if hc["cgroup_cpu_quota"] is None:
+        assert hc["threads"] == hc["affinity_cpus"]  # uncapped
+
+
+def test_roofline_refuses_pmc_of_another_build(grt, tmp_path, monkeypatch):
+    import bench
+
+    pmc = tmp_path / "pmc.json"
+    pmc.write_text(json.dumps({"code_object_sha256": "0" * 64, "hbm_bytes_per_launch": 1.0}))
+    monkeypatch.setitem(bench.PMC_FILE, "c2", pmc)
+    r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")
+    assert r["traffic"] is None and "another build" in r["traffic_note"]
+    assert abs(r["frac"] * bench.FP64_VECTOR_PEAK_TFLOPS - r["achieved"]) < 1e-9
+    assert abs(r["frac_no_contraction"] - 2 * r["frac"]) < 1e-12
+    pmc.write_text(json.dumps({"code_object_sha256": grt._lib.device_code_sha256(), "hbm_bytes_per_launch": 7.0,
+                               "lane_utilisation": 0.9}))
+    r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")
+    assert r["traffic"] == 7.0 and r["lane_utilisation"] == 0.9

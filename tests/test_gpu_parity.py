@@ -8,13 +8,13 @@ value), with identical class / status / stop reason.
 
 The device's libm (OCML) differs from glibc in the last ulp of sin/cos/pow, so the bar
 is applied relative to the oracle's own last-ulp sensitivity (check_parity): the oracle
-is re-run under 1-ulp probes of its pow() and of the RHS's sin()/cos(), and the GPU may
-disagree with it on no more pixels than those probes move.  Scenes without
+is re-run under 1-ulp probes of its pow() and of the RHS's sin()/cos(), and every pixel
+where the GPU disagrees with it must be one of the pixels those probes move.  Scenes without
 libm-sensitive pixels (C1, C2/C3 crops) are therefore held to every pixel.
 
 C4 (kerr.toml, Kerr-Schild) at the photon ring is chaotic: a
-1-ulp change of the oracle's pow() moves those pixels by up to ~20%, so C4 is held to
-class/stop identity, the per-pixel bar away from the ring, and a crop-mean bound.
+1-ulp change of the oracle's pow() moves those pixels by up to ~20%.  The device's pow
+is glibc's bit for bit, so the ring crop is held to every pixel and every step count.
 """
 import math
 
@@ -66,10 +66,11 @@ def agree(a_xyza, a_cls, ref):
 def check_parity(got, ref, probes, *, max_sensitive=0.02):
     """The parity bar on one batch of pixels (see module docstring):
 
-    * the GPU may disagree with the oracle (1e-4 per channel, or class) on no more
-      pixels than the union of the oracle's own last-ulp probes moves -- for a scene
-      with no libm-sensitive pixel that means every pixel agrees;
-    * class, status and stop reason are identical wherever all probes agree;
+    * every pixel where the GPU disagrees with the oracle (1e-4 per channel, or class)
+      must be one the oracle's own last-ulp probes move (``bad`` is a subset of
+      ``~robust``): a wrong *robust* pixel fails wherever it is -- for a scene with no
+      libm-sensitive pixel that means every pixel agrees;
+    * class, status and stop reason are identical on every robust pixel;
     * step counts agree at least as often as the oracle agrees with its probes (-1%)."""
     robust = np.ones(len(ref["ray_class"]), bool)
     for p in probes:
@@ -78,13 +79,15 @@ def check_parity(got, ref, probes, *, max_sensitive=0.02):
     assert n_sensitive <= max_sensitive * len(robust), f"{n_sensitive} pixels libm-sensitive"
     ok = agree(got.xyza64, got.ray_class, ref)
     bad = np.where(~ok)[0]
-    assert bad.size <= n_sensitive, f"{bad.size} pixels outside 1e-4 (oracle's own last-ulp spread: " \
-                                    f"{n_sensitive}), e.g. {bad[:5]}: {got.xyza64[bad[:3]]} vs {ref['xyza'][bad[:3]]}"
+    wrong_robust = np.where(~ok & robust)[0]
+    assert wrong_robust.size == 0, f"{wrong_robust.size} robust pixels outside 1e-4 (of {bad.size} disagreeing; " \
+        f"{n_sensitive} libm-sensitive), e.g. {wrong_robust[:5]}: {got.xyza64[wrong_robust[:3]]} vs " \
+        f"{ref['xyza'][wrong_robust[:3]]}"
+    assert bad.size <= n_sensitive
     # the f32 framebuffer is the f64 colour rounded once
     assert np.array_equal(got.xyza, got.xyza64.astype(np.float32))
-    both = robust & ok
     for key, mine in (("ray_class", got.ray_class), ("status", got.status), ("stop", got.stop_reason)):
-        assert np.array_equal(mine[both], ref[key][both]), key
+        assert np.array_equal(mine[robust], ref[key][robust]), key
     if got.steps is not None:
         same = np.mean(got.steps == ref["steps"])
         floor = min(np.mean(p["steps"] == ref["steps"]) for p in probes)
@@ -177,8 +180,12 @@ def test_c4_kerr_schild_off_ring(grt, oracle, gpu):
     check_parity(got, ref, probes)
 
 
-def test_c4_chaos_floor(grt, oracle, gpu):
-    """configs[3] at the photon ring: GPU-vs-oracle no worse than oracle-vs-oracle(1 ulp)."""
+def test_c4_photon_ring(grt, oracle, gpu):
+    """configs[3] at the photon ring.  The ring is chaotic for the
+    oracle itself -- a 1-ulp change of its pow() moves most of this crop by more than
+    1e-4 -- but the device restates glibc's pow / sin / cos / sincos bit for bit, so the
+    GPU follows the oracle's trajectories exactly: every pixel within 1e-4 with the
+    same class, status, stop reason and step count."""
     hs = host_scene(grt, "kerr.toml", c4_opts(grt))
     sc = gpu_scene(grt, hs)
     rect = (2000, 2000, 16, 16)
@@ -189,15 +196,13 @@ def test_c4_chaos_floor(grt, oracle, gpu):
         pert = oracle.render_pixels(hs.desc, *rect, threads=ORACLE_THREADS)
     finally:
         oracle.lib().oracle_set_libm_perturbation(0)
-    # the ring is chaotic for the oracle itself
-    assert within(pert["xyza"], ref["xyza"]).mean() < 0.5
+    assert within(pert["xyza"], ref["xyza"]).mean() < 0.5  # the chaos evidence
+    ok = within(got.xyza64, ref["xyza"])
+    assert ok.all(), f"{(~ok).sum()} of {ok.size} ring pixels outside 1e-4"
     assert np.array_equal(got.ray_class, ref["ray_class"])
-    assert np.mean(got.stop_reason == ref["stop"]) >= 0.99
-    assert np.mean(got.status == ref["status"]) >= 0.99
-    m_got, m_ref, m_pert = got.xyza64.mean(0), ref["xyza"].mean(0), pert["xyza"].mean(0)
-    pert_dev = np.abs(m_pert - m_ref) / np.abs(m_ref)
-    gpu_dev = np.abs(m_got - m_ref) / np.abs(m_ref)
-    assert np.all(gpu_dev <= np.maximum(10 * pert_dev, 1e-2)), (gpu_dev, pert_dev)
+    assert np.array_equal(got.status, ref["status"])
+    assert np.array_equal(got.stop_reason, ref["stop"])
+    assert np.array_equal(got.steps, ref["steps"])
 
 
 # ------------------------------------------------------------------ offsets mode --

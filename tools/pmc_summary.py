@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 --pmc passes of tools/run_pmc.sh for the integrate kernel.
 
-usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<tag>_pmc.json
+usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<name>_pmc.json [kernel] [workload text]
 Counter values are summed over the rows of each dispatch of grt::integrate_kernel<1>
 (one C2 frame per dispatch) and reported per launch.  FETCH_SIZE (KB) is doubled per
 the gfx950 correction in MI355X_MICROARCH.md; WRITE_SIZE (KB) is taken as is.
@@ -12,7 +12,11 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from gr_raytracer_amd._lib import device_code_sha256  # noqa: E402
+
 KERNEL = sys.argv[3] if len(sys.argv) > 3 else "grt::integrate_kernel<1, false>"
+WORKLOAD = sys.argv[4] if len(sys.argv) > 4 else "one frame of tools/prof_target.py c2 (1500x1500, 2.25M rays)"
 
 
 def load(pass_dir):
@@ -41,7 +45,9 @@ def main():
     fetch_b = counters.get("FETCH_SIZE", 0.0) * 1024 * 2
     write_b = counters.get("WRITE_SIZE", 0.0) * 1024
     out = {
-        "kernel": f"{KERNEL}, one frame of tools/prof_target.py (1500x1500, 2.25M rays)",
+        "kernel": f"{KERNEL}, {WORKLOAD}",
+        # the device code the passes measured: bench.py refuses a summary of another build
+        "code_object_sha256": device_code_sha256(),
         "source": "rocprofv3 --kernel-trace --pmc <one counter group per pass>, tools/run_pmc.sh",
         "counters": counters,
         "kernel_ms_per_pass": kernel_ms,
