@@ -9,9 +9,9 @@ mkdir -p "$OUT"
 KEXPR=${2:-}
 echo "[gpu_round] pytest -m gpu" >&2
 if [ -n "$KEXPR" ]; then
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rA -p no:cacheprovider --timeout 300 --timeout-method thread -k "$KEXPR" > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rA -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25 -k "$KEXPR" > "$OUT/pytest_gpu.log" 2>&1
 else
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rA -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rA -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25 > "$OUT/pytest_gpu.log" 2>&1
 fi
 rc=$?
 tail -5 "$OUT/pytest_gpu.log" >&2
