@@ -32,6 +32,7 @@
 //
 // Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fopenmp).
 
+#include <cerrno>
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -1780,6 +1781,8 @@ static double select_pixels(const std::vector<Sample>& buf, uint32_t w, uint32_t
   return min_lum;
 }
 
+#include "host_setup.inc"  // Camera::new, KerrTemperatureComputer::new, BlackBodyMapper::new
+
 }  // namespace oracle
 
 // =================================================================== C ABI =====
@@ -2222,6 +2225,27 @@ double oracle_select_pixels(const double* xyza, const uint8_t* cls, uint32_t w, 
   std::memset(flags_out, 0, n);
   for (uint64_t pi : sel) flags_out[pi] = 1;
   return min_lum;
+}
+// ---- host setup, restated (host_setup.inc) ----
+int oracle_camera_setup(int32_t geometry, double radius, double a, const double* cart, int velocity_mode,
+                        const double* explicit_velocity, double alpha, int64_t rows, int64_t cols, double phi,
+                        double theta, double psi, grt_camera_desc* out) {
+  return setup::camera_setup(geometry, radius, a, cart, velocity_mode, explicit_velocity, alpha, rows, cols, phi,
+                             theta, psi, out);
+}
+int oracle_kerr_temperature_lut(double temperature, double outer_radius, double a, double radius, uint32_t n,
+                                double* lut_r, double* lut_t, double* r_isco) {
+  if (n < 2) return -EINVAL;
+  return setup::kerr_temperature_lut(temperature, outer_radius, a, radius, n, lut_r, lut_t, r_isco);
+}
+double oracle_r_isco(double radius, double a) { return setup::r_isco(radius, a); }
+int oracle_blackbody_lut(uint32_t n, double* log_t, double* xyz) {
+  if (n < 2) return -EINVAL;
+  setup::blackbody_lut(n, log_t, xyz);
+  return 0;
+}
+void oracle_blackbody_xyz(double temperature, double redshift, double* out) {
+  setup::blackbody_xyz(temperature, redshift, out);
 }
 }  // extern "C"
 

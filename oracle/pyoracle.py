@@ -42,6 +42,13 @@ def lib():
                                             C.c_int]
         L.oracle_select_pixels.restype = _d
         L.oracle_select_pixels.argtypes = [_pd, _u8p, C.c_uint32, C.c_uint32, vp, _u8p]
+        L.oracle_camera_setup.argtypes = [C.c_int32, _d, _d, _pd, C.c_int, _pd, _d, C.c_int64, C.c_int64, _d, _d, _d,
+                                          vp]
+        L.oracle_kerr_temperature_lut.argtypes = [_d, _d, _d, _d, C.c_uint32, _pd, _pd, _pd]
+        L.oracle_r_isco.restype = _d
+        L.oracle_r_isco.argtypes = [_d, _d]
+        L.oracle_blackbody_lut.argtypes = [C.c_uint32, _pd, _pd]
+        L.oracle_blackbody_xyz.argtypes = [_d, _d, _pd]
         L.oracle_rk_analytic.argtypes = [_d, _pd, _pd]
         L.oracle_integrate_ray.restype = C.c_int64
         L.oracle_integrate_ray.argtypes = [vp, _pd, _pd, _pd, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -144,6 +151,43 @@ def select_pixels(xyza, cls, w, h, adaptive):
     min_lum = lib().oracle_select_pixels(_dp(x), c.ctypes.data_as(_u8p), w, h,
                                          C.cast(C.pointer(adaptive), C.c_void_p), flags.ctypes.data_as(_u8p))
     return flags.astype(bool), float(min_lum)
+
+
+# ---- host setup, restated (oracle/host_setup.inc) ----
+def camera_setup(camera_desc_type, geometry, radius, a, cart, velocity_mode=0, explicit=None, alpha=np.pi / 4,
+                 rows=500, cols=500, phi=0.0, theta=0.0, psi=0.0):
+    """Camera::new after the CLI's placement (main.rs:92-104, cli/<geometry>.rs,
+    cli/shared.rs:48-77): returns (rc, grt_camera_desc).  velocity_mode 0 static, 1 ZAMO,
+    2 explicit."""
+    out = camera_desc_type()
+    c = np.ascontiguousarray(cart, np.float64)
+    e = None if explicit is None else np.ascontiguousarray(explicit, np.float64)
+    rc = lib().oracle_camera_setup(geometry, radius, a, _dp(c), velocity_mode, _dp(e) if e is not None else None,
+                                   alpha, rows, cols, phi, theta, psi, C.cast(C.pointer(out), C.c_void_p))
+    return rc, out
+
+
+def kerr_temperature_lut(temperature, outer_radius, a, radius, n=1000):
+    r, t, ri = np.zeros(n), np.zeros(n), C.c_double()
+    rc = lib().oracle_kerr_temperature_lut(temperature, outer_radius, a, radius, n, _dp(r), _dp(t), C.byref(ri))
+    return rc, r, t, ri.value
+
+
+def r_isco(radius, a):
+    return lib().oracle_r_isco(radius, a)
+
+
+def blackbody_lut(n=1000):
+    lt, xyz = np.zeros(n), np.zeros((n, 3))
+    rc = lib().oracle_blackbody_lut(n, _dp(lt), _dp(xyz))
+    assert rc == 0
+    return lt, xyz
+
+
+def blackbody_xyz(temperature, redshift=1.0):
+    out = np.zeros(3)
+    lib().oracle_blackbody_xyz(temperature, redshift, _dp(out))
+    return out
 
 
 def rk_analytic(t_end):

@@ -205,6 +205,56 @@ def test_c4_photon_ring(grt, oracle, gpu):
     assert np.array_equal(got.steps, ref["steps"])
 
 
+def oracle_built_desc(grt, oracle, hs, toml):
+    """A copy of the product's descriptor with every host-built per-frame quantity
+    replaced by the oracle's own restatement (oracle/host_setup.inc): camera tetrad and
+    velocity, the Kerr temperature LUTs, the blackbody LUT.  Textures stay shared."""
+    import ctypes as C
+
+    import tomli
+
+    from conftest import SCENES
+
+    d = grt._lib.SceneDesc()
+    C.memmove(C.byref(d), C.byref(hs.desc), C.sizeof(d))
+    o = hs.opts
+    rc, cam = oracle.camera_setup(grt._lib.CameraDesc, int(d.geometry), float(d.radius), float(d.a),
+                                  tuple(o.camera_position), 0, alpha=math.pi / 4, rows=int(o.height),
+                                  cols=int(o.width), phi=float(o.phi), theta=float(o.theta), psi=float(o.psi))
+    assert rc == 0
+    d.camera = cam
+    keep = [hs]
+    cfg = tomli.loads((SCENES / toml).read_text())
+    for k in range(d.n_objects):
+        ob = d.objects[k]
+        if ob.temp_kind == grt._lib.TEMP_KERR_LUT:
+            spec = next(iter(cfg["objects"][k].values()))
+            rc, r, t, ri = oracle.kerr_temperature_lut(float(spec["temperature"]), float(spec["outer_radius"]),
+                                                        d.a, d.radius, int(ob.lut_n))
+            assert rc == 0
+            keep += [r, t]
+            ob.lut_r, ob.lut_t, ob.r_isco = grt._lib.dptr(r), grt._lib.dptr(t), ri
+    if d.bb_n:
+        lt, xyz = oracle.blackbody_lut(int(d.bb_n))
+        keep += [lt, xyz]
+        d.bb_log_t, d.bb_xyz = grt._lib.dptr(lt), grt._lib.dptr(xyz)
+    return d, keep
+
+
+@pytest.mark.parametrize("toml,opts_fn,rect", [("kerr-bl.toml", c3_opts, (734, 734, 32, 32)),
+                                               ("kerr.toml", c4_opts, (1000, 1000, 16, 16))])
+def test_oracle_built_descriptor(grt, oracle, gpu, toml, opts_fn, rect):
+    """GPU vs oracle on a descriptor whose camera and LUTs come from the oracle's own
+    restatement of the host setup (not from csrc/host/setup.cpp)."""
+    hs = host_scene(grt, toml, opts_fn(grt))
+    d, keep = oracle_built_desc(grt, oracle, hs, toml)
+    sc = grt.Scene(_desc_ptr(d), keepalive=(d, keep))
+    got = sc.render_pixels(*rect)
+    ref, probes = oracle_pair(oracle, d, *rect)
+    check_parity(got, ref, probes)
+    assert (got.ray_class == grt._lib.CLASS_HIT).sum() > 0  # the crop shows the BlackBody disc
+
+
 # ------------------------------------------------------------------ offsets mode --
 def test_offsets_mode_matches_oracle(grt, oracle, gpu):
     """Explicit (pixel, dx, dy) lists: the adaptive resampling entry (raytracer.rs:460-525)."""
