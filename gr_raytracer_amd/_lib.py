@@ -112,6 +112,11 @@ class RowShard(C.Structure):
     _fields_ = [("band_rows", C.c_uint32), ("shard", C.c_uint32), ("n_shards", C.c_uint32)]
 
 
+class SubsampleFailures(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("pixel", C.POINTER(C.c_uint32)), ("sample", C.POINTER(C.c_uint32)),
+                ("status", C.POINTER(C.c_uint8)), ("count", C.c_uint64)]
+
+
 class GrtError(RuntimeError):
     pass
 
@@ -187,6 +192,12 @@ def lib() -> C.CDLL:
                                                         C.POINTER(_d)]),
         "grt_supersample_shard": (C.c_int, [vp, C.c_int, vp, C.POINTER(RowShard), C.POINTER(AdaptiveConfig), _d, vp, vp,
                                             _pd, vp, C.POINTER(C.c_uint64), vp]),
+        "grt_supersample_shard_device": (C.c_int, [vp, C.c_int, vp, C.POINTER(RowShard), C.POINTER(AdaptiveConfig), _d,
+                                                   vp, vp, vp, _pd, vp, vp, vp, C.POINTER(SubsampleFailures)]),
+        "grt_adaptive_floor_device": (C.c_int, [vp, C.c_int, vp, vp, u32, u64, vp]),
+        "grt_render_section_ex": (C.c_int, [vp, C.c_int, u32, u32, u32, u32, C.POINTER(AdaptiveConfig), _pd, _pd,
+                                            C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(Stats),
+                                            C.POINTER(C.c_uint8), C.POINTER(SubsampleFailures)]),
         "grt_write_png_rgb": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), u32, u32]),
         "grt_write_hdr_xyz": (C.c_int, [C.c_char_p, _pd, u32, u32]),
         "grt_linear_max_async": (C.c_int, [C.c_int, vp, vp, u64, _d, vp]),
@@ -223,6 +234,7 @@ EXPORTED_SYMBOLS = [
     "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",
     "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_adaptive_min_luminance_device", "grt_supersample_shard",
+    "grt_supersample_shard_device", "grt_adaptive_floor_device", "grt_render_section_ex",
     "grt_write_png_rgb", "grt_write_hdr_xyz",
 ]
 

@@ -16,6 +16,7 @@
 // Global options go before the subcommand, subcommand options after it (clap).
 // Extra (not in the reference): --device N selects the GPU, --resource-root DIR
 // resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -372,8 +373,13 @@ int main(int argc, char** argv) {
   grt_stats st;
   uint64_t nsel = 0;
   std::vector<uint8_t> status((size_t)w * h);
-  if (grt_render_section(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st,
-                         status.data())) {
+  // failed supersample sub-rays (raytracer.rs:357-362), up to 1M logged
+  const uint64_t fail_cap = 1u << 20;
+  std::vector<uint32_t> fail_pix(fail_cap), fail_sample(fail_cap);
+  std::vector<uint8_t> fail_status(fail_cap);
+  grt_subsample_failures fails{fail_cap, fail_pix.data(), fail_sample.data(), fail_status.data(), 0};
+  if (grt_render_section_ex(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st,
+                            status.data(), &fails)) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
@@ -383,6 +389,13 @@ int main(int argc, char** argv) {
     if (status[i] & 0x7f)
       std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n",
                    (unsigned)(c0 + i % w), (unsigned)(r0 + i / w), error_debug_name(status[i] & 0x7f));
+  // :357-362: the same message for each failed sub-sample ray of a supersampled pixel
+  for (uint64_t k = 0; k < std::min<uint64_t>(fails.count, fail_cap); ++k)
+    std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n",
+                 (unsigned)(c0 + fail_pix[k] % w), (unsigned)(r0 + fail_pix[k] / w), error_debug_name(fail_status[k]));
+  if (fails.count > fail_cap)
+    std::fprintf(stderr, "[grt] ERROR %llu more failed sub-sample rays not listed\n",
+                 (unsigned long long)(fails.count - fail_cap));
   std::fprintf(stderr, "[grt] %llu rays, %llu accepted steps, %llu attempts, %llu supersampled pixels, kernel %.1f ms "
                "(%.3e steps/s)\n",
                (unsigned long long)st.rays, (unsigned long long)st.accepted_steps, (unsigned long long)st.attempts,

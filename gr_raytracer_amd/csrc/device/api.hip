@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -63,6 +64,10 @@ struct DeviceCopy {
   // tile-order scratch (probe counts, keys, indices, order, radix-sort temp), grow-only
   uint64_t sched_tiles = 0;
   void* sched_mem = nullptr;
+  // adaptive-pass scratch (section buffers, flags, selection, sort and sub-ray buffers),
+  // grow-only: no allocation (and no implicit device synchronisation) between passes
+  uint64_t ad_bytes = 0;
+  void* ad_mem = nullptr;
 };
 
 // Carve a Workspace for n rays out of the device's grow-only arena.
@@ -107,6 +112,7 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   ws->rec_dir = ws->vcol = nullptr;
   ws->jobs = nullptr;
   ws->march = dc.d_march;
+  ws->n_live = nullptr;
   if (vol) {
     ws->rec_dir = (double*)take(3 * M * 8 * cap);
     ws->vcol = (double*)take(4 * M * 8 * cap);
@@ -438,6 +444,7 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   grt::Workspace ws;
   int rc = ensure_workspace(dc, n_out, &ws);
   if (rc) return rc;
+  ws.n_live = wl.n_live;
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
                             dc.vol, stream));
   return 0;
@@ -552,6 +559,7 @@ int grt_scene_destroy(grt_scene* s) {
     for (void* p : dc->allocations) (void)hipFree(p);
     if (dc->ws_mem) (void)hipFree(dc->ws_mem);
     if (dc->sched_mem) (void)hipFree(dc->sched_mem);
+    if (dc->ad_mem) (void)hipFree(dc->ad_mem);
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
     delete dc;
@@ -727,6 +735,94 @@ int grt_trace_rays(grt_scene* s, int device, uint64_t n, const double* positions
                       status_out);
 }
 
+// ------------------------------------------------------------- adaptive pass ----
+// Bump allocator over the device's grow-only adaptive arena.  Plan the whole call's
+// buffers first (ad_plan), then carve them (ad_take): growing the arena happens before
+// any kernel of the call is enqueued.
+struct AdArena {
+  char* base = nullptr;
+  uint64_t off = 0;
+  void* take(uint64_t bytes) {
+    void* r = base ? base + off : nullptr;
+    off += (bytes + 255) & ~255ull;
+    return r;
+  }
+};
+static int ad_reserve(DeviceCopy& dc, uint64_t bytes) {
+  if (bytes <= dc.ad_bytes && dc.ad_mem) return 0;
+  if (dc.ad_mem) {
+    (void)hipDeviceSynchronize();  // earlier async launches may still use the old arena
+    (void)hipFree(dc.ad_mem);
+    dc.ad_mem = nullptr;
+    dc.ad_bytes = 0;
+  }
+  const uint64_t cap = bytes + (bytes >> 3);
+  if (hipMalloc(&dc.ad_mem, cap) != hipSuccess) return fail(-ENOMEM, "cannot allocate the adaptive-pass scratch");
+  dc.ad_bytes = cap;
+  return 0;
+}
+
+constexpr uint64_t SUB_CHUNK = 1ull << 21;  // sub-rays per supersample trace launch
+
+// Buffers of the supersample pass over at most n_max selected pixels.
+struct SuperBufs {
+  uint64_t chunk_pix = 0, cap = 0;
+  uint32_t n_chunks = 0, per = 0;
+  uint32_t* pix = nullptr;
+  double *dx = nullptr, *dy = nullptr, *x64 = nullptr;
+  float* xyza = nullptr;
+  uint8_t *cls = nullptr, *status = nullptr;
+  unsigned long long* live = nullptr;
+  void carve(AdArena& A, uint64_t n_max, uint32_t spa) {
+    per = spa * spa;
+    chunk_pix = std::max<uint64_t>(1, std::min<uint64_t>(n_max, SUB_CHUNK / per));
+    n_chunks = (uint32_t)((n_max + chunk_pix - 1) / chunk_pix);
+    cap = chunk_pix * per;
+    pix = (uint32_t*)A.take(cap * 4);
+    dx = (double*)A.take(cap * 8);
+    dy = (double*)A.take(cap * 8);
+    xyza = (float*)A.take(cap * 16);
+    cls = (uint8_t*)A.take(cap);
+    status = (uint8_t*)A.take(cap);
+    x64 = (double*)A.take(cap * 32);
+    live = (unsigned long long*)A.take((uint64_t)n_chunks * 8);
+  }
+};
+
+// supersample (raytracer.rs:320-384) over a selection that lives on the device: entries
+// j < *d_count <= n_max of sel_px (pixel index in the rect row0/col0/rows/cols: camera
+// ray and jitter hash) and sel_out (index into d_out64).  The sub-rays go through the
+// trace in chunks of SUB_CHUNK; the integrate / shade kernels read each chunk's live
+// count from the device, so nothing waits for the host between the passes.
+static int enqueue_supersample(grt_scene* s, DeviceCopy& dc, hipStream_t st, const SuperBufs& B, uint32_t row0,
+                        uint32_t col0, uint32_t rows, uint32_t cols, const uint32_t* sel_px, const uint32_t* sel_out,
+                        const unsigned long long* d_count, uint32_t spa, double* d_out64, unsigned long long* d_stats,
+                        const grt::SubsampleFailures& fails) {
+  HIP_TRY(grt::launch_chunk_live(d_count, B.n_chunks, B.chunk_pix, B.per, B.live, st));
+  for (uint32_t c = 0; c < B.n_chunks; ++c) {
+    const uint64_t base = (uint64_t)c * B.chunk_pix;
+    HIP_TRY(grt::launch_make_offsets(sel_px + base, B.chunk_pix, d_count, base, spa, row0, col0, cols, B.pix, B.dx,
+                                     B.dy, st));
+    grt::WorkList wo;
+    std::memset(&wo, 0, sizeof(wo));
+    wo.row0 = row0;
+    wo.col0 = col0;
+    wo.rows = rows;
+    wo.cols = cols;
+    wo.n_items = B.cap;
+    wo.pixel_index = B.pix;
+    wo.dx = B.dx;
+    wo.dy = B.dy;
+    wo.n_live = B.live + c;
+    grt::Outputs so{B.xyza, B.cls, B.status, B.x64, nullptr, nullptr};
+    int rc = enqueue_trace(s, dc, wo, so, d_stats, st);
+    if (rc) return rc;
+    HIP_TRY(grt::launch_average(sel_out + base, sel_px + base, B.chunk_pix, d_count, base, spa, B.x64, B.status,
+                                d_out64, fails, st));
+  }
+  return 0;
+}
+
 // resolve_minimum_luminance's relative floor (raytracer.rs:118-129): 1e-3 x the element
 // at ((n - 1) * 0.99) as usize in f64::total_cmp order (select_nth_unstable_by selects
 // the same element as nth_element under the same total order).  Reorders `lum`.
@@ -742,25 +838,7 @@ static double relative_min_luminance(std::vector<double>& lum) {
   return 1e-3 * lum[index];
 }
 
-// relative_min_luminance of n device luminances d_y[stride * i], selected on the device
-// (radix sort in f64::total_cmp order): the same element, without the host copy.
-static int device_relative_min_luminance(const double* d_y, uint32_t stride, uint64_t n, hipStream_t st,
-                                         double* out) {
-  if (n == 0) {
-    *out = 0.0;
-    return 0;
-  }
-  const uint64_t index = (uint64_t)((double)(n - 1) * 0.99);
-  size_t bytes = 0;
-  HIP_TRY(grt::luminance_order_stat(d_y, stride, n, index, nullptr, &bytes, nullptr, st));
-  DevBuf b_sort;
-  int rc = b_sort.alloc(bytes);
-  if (rc) return rc;
-  double v = 0.0;
-  HIP_TRY(grt::luminance_order_stat(d_y, stride, n, index, b_sort.p, &bytes, &v, st));
-  *out = 1e-3 * v;
-  return 0;
-}
+static uint64_t floor_index(uint64_t n) { return (uint64_t)((double)(n - 1) * 0.99); }
 
 int grt_adaptive_min_luminance_device(int device, void* stream, const double* d_y, uint32_t stride, uint64_t n,
                                       const grt_adaptive_config* cfg, double* out) {
@@ -769,8 +847,21 @@ int grt_adaptive_min_luminance_device(int device, void* stream, const double* d_
     *out = cfg->minimum_luminance;
     return 0;
   }
+  if (n == 0) {
+    *out = 0.0;
+    return 0;
+  }
+  if (n > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "more than INT_MAX luminances");
   HIP_TRY(hipSetDevice(device));
-  return device_relative_min_luminance(d_y, stride, n, (hipStream_t)stream, out);
+  size_t bytes = 0;
+  HIP_TRY(grt::luminance_order_stat(d_y, stride, n, floor_index(n), nullptr, &bytes, nullptr, (hipStream_t)stream));
+  DevBuf b;
+  int rc = b.alloc(bytes);
+  if (rc) return rc;
+  double v = 0.0;
+  HIP_TRY(grt::luminance_order_stat(d_y, stride, n, floor_index(n), b.p, &bytes, &v, (hipStream_t)stream));
+  *out = 1e-3 * v;
+  return 0;
 }
 
 double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adaptive_config* cfg) {
@@ -780,10 +871,31 @@ double grt_adaptive_min_luminance(const double* lum, uint64_t n, const grt_adapt
   return relative_min_luminance(v);
 }
 
-int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
-                       uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza,
-                       double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats,
-                       uint8_t* status_out) {
+// The recorded failed sub-samples, sorted by (pixel, stratum): the reference logs them
+// from a parallel loop (raytracer.rs:357-362), in no particular order.
+static int copy_failures(const grt::SubsampleFailures& f, uint64_t count, uint32_t spa, grt_subsample_failures* out) {
+  const uint64_t m = std::min<uint64_t>(count, f.cap);
+  if (m == 0) return 0;
+  std::vector<uint64_t> key(m);
+  std::vector<uint8_t> st(m);
+  HIP_TRY(hipMemcpy(key.data(), f.key, m * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(st.data(), f.status, m, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> order(m);
+  for (uint64_t i = 0; i < m; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return key[a] < key[b]; });
+  const uint64_t per = (uint64_t)spa * spa;
+  for (uint64_t i = 0; i < m; ++i) {
+    out->pixel[i] = (uint32_t)(key[order[i]] / per);
+    if (out->sample) out->sample[i] = (uint32_t)(key[order[i]] % per);
+    out->status[i] = st[order[i]];
+  }
+  return 0;
+}
+
+int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
+                          uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza, double* xyza_out,
+                          uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats, uint8_t* status_out,
+                          grt_subsample_failures* failures) {
   if (!s || !cfg || !xyza_out) return fail(-EINVAL, "null argument");
   if (to_row < from_row || to_col < from_col) return fail(-EINVAL, "empty section");
   if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
@@ -798,82 +910,97 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
   uint64_t n = (uint64_t)w * h;
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (n_supersampled) *n_supersampled = 0;
+  if (failures) failures->count = 0;
   if (n == 0) return 0;
+  const bool supersampled = cfg->enabled || mask_xyza != nullptr;
+  const bool device_floor = supersampled && !cfg->has_minimum_luminance;
+  if (supersampled && n > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "section larger than INT_MAX pixels");
+  const uint32_t spa = cfg->samples_per_axis;
+  // plan: section buffers, selection, floor, sort / compaction scratch, sub-ray buffers
+  size_t sort_bytes = 0, select_bytes = 0;
+  if (device_floor) HIP_TRY(grt::luminance_floor_device(nullptr, 4, n, floor_index(n), nullptr, &sort_bytes, nullptr, 0));
+  if (supersampled) HIP_TRY(grt::compact_flags(nullptr, n, nullptr, nullptr, nullptr, &select_bytes, 0));
+  const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
+  grt::SubsampleFailures fails{nullptr, nullptr, nullptr, fail_cap};
+  auto carve = [&](AdArena& A, float** xyza, uint8_t** cls, uint8_t** status, double** x64, uint8_t** flags,
+                   uint32_t** sel, unsigned long long** cnt, double** floor, void** sort, void** select,
+                   SuperBufs* B) {
+    *xyza = (float*)A.take(n * 16);
+    *cls = (uint8_t*)A.take(n);
+    *status = (uint8_t*)A.take(n);
+    *x64 = (double*)A.take(n * 32);
+    if (!supersampled) return;
+    *flags = (uint8_t*)A.take(n);
+    *sel = (uint32_t*)A.take(n * 4);
+    *cnt = (unsigned long long*)A.take(16);  // [0] selected pixels, [1] failed sub-samples
+    *floor = (double*)A.take(8);
+    *sort = A.take(sort_bytes);
+    *select = A.take(select_bytes);
+    if (!mask_xyza) B->carve(A, n, spa);
+    fails.key = (uint64_t*)A.take(fail_cap * 8);
+    fails.status = (uint8_t*)A.take(fail_cap);
+  };
+  float* b_xyza = nullptr;
+  uint8_t *b_cls = nullptr, *b_status = nullptr, *b_flags = nullptr;
+  double *b_x64 = nullptr, *d_floor = nullptr;
+  uint32_t* b_sel = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  void *b_sort = nullptr, *b_select = nullptr;
+  SuperBufs B;
+  {
+    AdArena plan;
+    carve(plan, &b_xyza, &b_cls, &b_status, &b_x64, &b_flags, &b_sel, &d_cnt, &d_floor, &b_sort, &b_select, &B);
+    if ((rc = ad_reserve(*dc, plan.off))) return rc;
+    AdArena A{(char*)dc->ad_mem, 0};
+    carve(A, &b_xyza, &b_cls, &b_status, &b_x64, &b_flags, &b_sel, &d_cnt, &d_floor, &b_sort, &b_select, &B);
+  }
   hipStream_t st = nullptr;
-  DevBuf b_xyza, b_cls, b_status, b_x64;
-  if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n)) || (rc = b_x64.alloc(n * 32)))
-    return rc;
   HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
   HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
+  if (supersampled) HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, st));
   HIP_TRY(hipEventRecord(dc->ev0, st));
   grt::WorkList wl = rect_worklist(from_row, from_col, h, w);
-  grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p, nullptr, nullptr};
+  grt::Outputs o{b_xyza, b_cls, b_status, b_x64, nullptr, nullptr};
   if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
-  bool supersampled = cfg->enabled || mask_xyza != nullptr;
-  uint64_t n_sel = 0;
   if (supersampled) {
-    // resolve_minimum_luminance (raytracer.rs:118-129): exact 99th percentile in
-    // f64::total_cmp order, selected on the host from the device 1-spp buffer.
-    double min_lum = cfg->minimum_luminance;
-    if (!cfg->has_minimum_luminance &&
-        (rc = device_relative_min_luminance((const double*)b_x64.p + 1, 4, n, st, &min_lum)))
-      return rc;
+    // resolve_minimum_luminance (raytracer.rs:118-129): the exact 99th percentile in
+    // f64::total_cmp order, selected on the device from the 1-spp buffer
+    if (device_floor)
+      HIP_TRY(grt::luminance_floor_device(b_x64 + 1, 4, n, floor_index(n), b_sort, &sort_bytes, d_floor, st));
     grt::AdaptiveParams ap;
     ap.w = w;
     ap.h = h;
     ap.exclude_background_contrast = cfg->exclude_background_contrast;
-    ap.min_lum = min_lum;
+    ap.min_lum = cfg->minimum_luminance;
     ap.luminance_contrast_threshold = cfg->luminance_contrast_threshold;
     ap.opacity_contrast_threshold = cfg->opacity_contrast_threshold;
-    DevBuf b_flags;
-    if ((rc = b_flags.alloc(n))) return rc;
-    HIP_TRY(grt::launch_select((const double*)b_x64.p, (const uint8_t*)b_cls.p, ap, (uint8_t*)b_flags.p, st));
-    std::vector<uint8_t> flags(n);
-    HIP_TRY(hipMemcpy(flags.data(), b_flags.p, n, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> sel;
-    for (uint64_t i = 0; i < n; ++i)
-      if (flags[i]) sel.push_back((uint32_t)i);
-    n_sel = sel.size();
-    if (n_sel) {
-      DevBuf b_sel;
-      if ((rc = b_sel.alloc(n_sel * 4))) return rc;
-      HIP_TRY(hipMemcpy(b_sel.p, sel.data(), n_sel * 4, hipMemcpyHostToDevice));
-      if (mask_xyza) {
-        HIP_TRY(grt::launch_paint((const uint32_t*)b_sel.p, n_sel, mask_xyza, (double*)b_x64.p, st));
-      } else {
-        uint32_t spa = cfg->samples_per_axis;
-        uint64_t ns = n_sel * spa * spa;
-        DevBuf b_pix, b_dx, b_dy, s_xyza, s_cls, s_status, s_x64;
-        if ((rc = b_pix.alloc(ns * 4)) || (rc = b_dx.alloc(ns * 8)) || (rc = b_dy.alloc(ns * 8)) ||
-            (rc = s_xyza.alloc(ns * 16)) || (rc = s_cls.alloc(ns)) || (rc = s_status.alloc(ns)) ||
-            (rc = s_x64.alloc(ns * 32)))
-          return rc;
-        HIP_TRY(grt::launch_make_offsets((const uint32_t*)b_sel.p, n_sel, spa, from_row, from_col, w,
-                                         (uint32_t*)b_pix.p, (double*)b_dx.p, (double*)b_dy.p, st));
-        grt::WorkList wo;
-        std::memset(&wo, 0, sizeof(wo));
-        wo.row0 = from_row;
-        wo.col0 = from_col;
-        wo.rows = h;
-        wo.cols = w;
-        wo.n_items = ns;
-        wo.pixel_index = (const uint32_t*)b_pix.p;
-        wo.dx = (const double*)b_dx.p;
-        wo.dy = (const double*)b_dy.p;
-        grt::Outputs so{(float*)s_xyza.p, (uint8_t*)s_cls.p, (uint8_t*)s_status.p, (double*)s_x64.p, nullptr, nullptr};
-        if ((rc = enqueue_trace(s, *dc, wo, so, dc->d_stats, st))) return rc;
-        HIP_TRY(grt::launch_average((const uint32_t*)b_sel.p, n_sel, spa, (const double*)s_x64.p,
-                                    (const uint8_t*)s_status.p, (double*)b_x64.p, st));
-        HIP_TRY(hipStreamSynchronize(st));
-      }
+    // collect_pixels_to_supersample (:386-458): stencil, then the selected pixels in
+    // order by a device stream compaction
+    HIP_TRY(grt::launch_select(b_x64, b_cls, ap, device_floor ? d_floor : nullptr, b_flags, st));
+    HIP_TRY(grt::compact_flags(b_flags, n, b_sel, d_cnt, b_select, &select_bytes, st));
+    if (mask_xyza) {  // raytracer.rs:285-295: paint instead of supersampling
+      HIP_TRY(grt::launch_paint(b_sel, n, d_cnt, mask_xyza, b_x64, st));
+    } else {
+      fails.count = d_cnt + 1;
+      if ((rc = enqueue_supersample(s, *dc, st, B, from_row, from_col, h, w, b_sel, b_sel, d_cnt, spa, b_x64,
+                                    dc->d_stats, fails)))
+        return rc;
     }
   }
   HIP_TRY(hipEventRecord(dc->ev1, st));
   HIP_TRY(hipEventSynchronize(dc->ev1));
-  HIP_TRY(hipMemcpy(xyza_out, b_x64.p, n * 32, hipMemcpyDeviceToHost));
-  if (class_out) HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
-  if (status_out) HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
-  if (n_supersampled) *n_supersampled = n_sel;
+  HIP_TRY(hipMemcpy(xyza_out, b_x64, n * 32, hipMemcpyDeviceToHost));
+  if (class_out) HIP_TRY(hipMemcpy(class_out, b_cls, n, hipMemcpyDeviceToHost));
+  if (status_out) HIP_TRY(hipMemcpy(status_out, b_status, n, hipMemcpyDeviceToHost));
+  if (supersampled) {
+    unsigned long long cnt[2] = {0, 0};
+    HIP_TRY(hipMemcpy(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (n_supersampled) *n_supersampled = cnt[0];
+    if (failures) {
+      failures->count = cnt[1];
+      if (int frc = copy_failures(fails, cnt[1], spa, failures)) return frc;
+    }
+  }
   if (stats) {
     unsigned long long hs[4];
     HIP_TRY(hipMemcpy(hs, dc->d_stats, sizeof(hs), hipMemcpyDeviceToHost));
@@ -892,6 +1019,14 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
     stats->march_emit_samples = m[5];
   }
   return 0;
+}
+
+int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
+                       uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza,
+                       double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats,
+                       uint8_t* status_out) {
+  return grt_render_section_ex(s, device, from_row, from_col, to_row, to_col, cfg, mask_xyza, xyza_out, class_out,
+                               n_supersampled, stats, status_out, nullptr);
 }
 
 
@@ -960,24 +1095,57 @@ int grt_render_shard_async(grt_scene* s, int device, void* stream, const grt_row
   return enqueue_trace(s, *dc, wl, o, (unsigned long long*)d_stats, (hipStream_t)stream);
 }
 
-int grt_supersample_shard(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
-                          const grt_adaptive_config* cfg, double min_lum, const double* d_frame_ya,
-                          const uint8_t* d_frame_class, const double* sampling_mask_xyza, double* d_xyza64,
-                          uint64_t* n_supersampled, uint64_t* d_stats) {
+int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
+                                 const grt_adaptive_config* cfg, double min_lum, const double* d_min_lum,
+                                 const double* d_frame_ya, const uint8_t* d_frame_class,
+                                 const double* sampling_mask_xyza, double* d_xyza64,
+                                 uint64_t* d_n_supersampled, uint64_t* d_stats, grt_subsample_failures* failures) {
   if (!s || !cfg || !d_frame_ya || !d_frame_class || !d_xyza64 || !d_stats) return fail(-EINVAL, "null argument");
   if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
   int rc = check_shard(sh);
   if (rc) return rc;
-  if (n_supersampled) *n_supersampled = 0;
+  if (failures) failures->count = 0;
   const uint32_t frame_rows = (uint32_t)s->desc.camera.rows, w = (uint32_t)s->desc.camera.cols;
   const uint32_t local_rows = grt_shard_row_count(frame_rows, sh);
   const uint64_t n_local = (uint64_t)local_rows * w;
-  if (n_local == 0) return 0;
   DeviceCopy* dc;
   if ((rc = ensure_device(s, device, &dc))) return rc;
   std::lock_guard<std::mutex> lk(dc->mu);
   HIP_TRY(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
+  if (n_local == 0) {
+    if (d_n_supersampled) HIP_TRY(hipMemsetAsync(d_n_supersampled, 0, 8, st));
+    return 0;
+  }
+  if (n_local > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "shard larger than INT_MAX pixels");
+  const uint32_t spa = cfg->samples_per_axis;
+  const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
+  size_t select_bytes = 0;
+  HIP_TRY(grt::compact_flags(nullptr, n_local, nullptr, nullptr, nullptr, &select_bytes, 0));
+  uint8_t* b_flags = nullptr;
+  uint32_t *sel_local = nullptr, *sel_frame = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  void* b_select = nullptr;
+  SuperBufs B;
+  grt::SubsampleFailures fails{nullptr, nullptr, nullptr, fail_cap};
+  auto carve = [&](AdArena& A) {
+    b_flags = (uint8_t*)A.take(n_local);
+    sel_local = (uint32_t*)A.take(n_local * 4);
+    sel_frame = (uint32_t*)A.take(n_local * 4);
+    d_cnt = (unsigned long long*)A.take(16);  // [0] selected pixels, [1] failed sub-samples
+    b_select = A.take(select_bytes);
+    if (!sampling_mask_xyza) B.carve(A, n_local, spa);
+    fails.key = (uint64_t*)A.take(fail_cap * 8);
+    fails.status = (uint8_t*)A.take(fail_cap);
+  };
+  {
+    AdArena plan;
+    carve(plan);
+    if ((rc = ad_reserve(*dc, plan.off))) return rc;
+    AdArena A{(char*)dc->ad_mem, 0};
+    carve(A);
+  }
+  HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, st));
   // collect_pixels_to_supersample (raytracer.rs:386-458) over this shard's pixels, with
   // the whole frame's 1-spp buffer as the neighbourhood
   grt::AdaptiveParams ap;
@@ -987,56 +1155,76 @@ int grt_supersample_shard(grt_scene* s, int device, void* stream, const grt_row_
   ap.min_lum = min_lum;
   ap.luminance_contrast_threshold = cfg->luminance_contrast_threshold;
   ap.opacity_contrast_threshold = cfg->opacity_contrast_threshold;
-  DevBuf b_flags;
-  if ((rc = b_flags.alloc(n_local))) return rc;
-  HIP_TRY(grt::launch_select_shard(d_frame_ya, d_frame_class, ap, sh->band_rows, sh->shard, sh->n_shards, local_rows,
-                                   (uint8_t*)b_flags.p, st));
-  std::vector<uint8_t> flags(n_local);
-  HIP_TRY(hipMemcpyAsync(flags.data(), b_flags.p, n_local, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  // selected pixels in frame order (shard rows increase with local rows): frame index for
-  // the jitter hash and the camera ray, local index for the output
-  std::vector<uint32_t> sel_frame, sel_local;
-  for (uint64_t i = 0; i < n_local; ++i)
-    if (flags[i]) {
-      uint64_t row = grt::shard_frame_row(sh->band_rows, sh->shard, sh->n_shards, (uint32_t)(i / w));
-      sel_frame.push_back((uint32_t)(row * w + i % w));
-      sel_local.push_back((uint32_t)i);
-    }
-  const uint64_t n_sel = sel_local.size();
-  if (n_supersampled) *n_supersampled = n_sel;
-  if (n_sel == 0) return 0;
-  DevBuf b_sel_frame, b_sel_local;
-  if ((rc = b_sel_frame.alloc(n_sel * 4)) || (rc = b_sel_local.alloc(n_sel * 4))) return rc;
-  HIP_TRY(hipMemcpyAsync(b_sel_local.p, sel_local.data(), n_sel * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(grt::launch_select_shard(d_frame_ya, d_frame_class, ap, d_min_lum, sh->band_rows, sh->shard, sh->n_shards,
+                                   local_rows, b_flags, st));
+  // selected pixels in frame order (shard rows increase with local rows): local index
+  // for the output, frame index for the jitter hash and the camera ray
+  HIP_TRY(grt::compact_flags(b_flags, n_local, sel_local, d_cnt, b_select, &select_bytes, st));
+  HIP_TRY(grt::launch_frame_index(sel_local, d_cnt, n_local, w, sh->band_rows, sh->shard, sh->n_shards, sel_frame,
+                                  st));
   if (sampling_mask_xyza) {  // raytracer.rs:285-295: paint instead of supersampling
-    HIP_TRY(grt::launch_paint((const uint32_t*)b_sel_local.p, n_sel, sampling_mask_xyza, d_xyza64, st));
+    HIP_TRY(grt::launch_paint(sel_local, n_local, d_cnt, sampling_mask_xyza, d_xyza64, st));
+  } else {
+    fails.count = d_cnt + 1;
+    if ((rc = enqueue_supersample(s, *dc, st, B, 0, 0, frame_rows, w, sel_frame, sel_local, d_cnt, spa, d_xyza64,
+                                  (unsigned long long*)d_stats, fails)))
+      return rc;
+  }
+  if (d_n_supersampled) HIP_TRY(hipMemcpyAsync(d_n_supersampled, d_cnt, 8, hipMemcpyDeviceToDevice, st));
+  if (failures) {
+    unsigned long long cnt[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    failures->count = cnt[1];
+    if ((rc = copy_failures(fails, cnt[1], spa, failures))) return rc;
+  }
+  return 0;
+}
+
+int grt_supersample_shard(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
+                          const grt_adaptive_config* cfg, double min_lum, const double* d_frame_ya,
+                          const uint8_t* d_frame_class, const double* sampling_mask_xyza, double* d_xyza64,
+                          uint64_t* n_supersampled, uint64_t* d_stats) {
+  if (n_supersampled) *n_supersampled = 0;
+  if (!s) return fail(-EINVAL, "null argument");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  DevBuf cnt;
+  if ((rc = cnt.alloc(8))) return rc;
+  HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, (hipStream_t)stream));
+  if ((rc = grt_supersample_shard_device(s, device, stream, sh, cfg, min_lum, nullptr, d_frame_ya, d_frame_class,
+                                         sampling_mask_xyza, d_xyza64, (uint64_t*)cnt.p, d_stats, nullptr)))
+    return rc;
+  uint64_t v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, cnt.p, 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  if (n_supersampled) *n_supersampled = v;
+  return 0;
+}
+
+// The luminance floor written to device memory (no host round trip): the multi-GPU
+// adaptive pass hands it to grt_supersample_shard_device.  Scratch from the scene's
+// grow-only arena on `device`, stream-ordered.
+int grt_adaptive_floor_device(grt_scene* s, int device, void* stream, const double* d_y, uint32_t stride, uint64_t n,
+                              double* d_min_lum) {
+  if (!s || !d_min_lum || (n && (!d_y || stride == 0))) return fail(-EINVAL, "null argument");
+  if (n > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "more than INT_MAX luminances");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    HIP_TRY(hipMemsetAsync(d_min_lum, 0, 8, st));  // +0.0
     return 0;
   }
-  HIP_TRY(hipMemcpyAsync(b_sel_frame.p, sel_frame.data(), n_sel * 4, hipMemcpyHostToDevice, st));
-  // supersample (raytracer.rs:320-384): samples_per_axis^2 jittered rays per pixel
-  const uint32_t spa = cfg->samples_per_axis;
-  const uint64_t ns = n_sel * spa * spa;
-  DevBuf b_pix, b_dx, b_dy, s_xyza, s_cls, s_status, s_x64;
-  if ((rc = b_pix.alloc(ns * 4)) || (rc = b_dx.alloc(ns * 8)) || (rc = b_dy.alloc(ns * 8)) ||
-      (rc = s_xyza.alloc(ns * 16)) || (rc = s_cls.alloc(ns)) || (rc = s_status.alloc(ns)) || (rc = s_x64.alloc(ns * 32)))
-    return rc;
-  HIP_TRY(grt::launch_make_offsets((const uint32_t*)b_sel_frame.p, n_sel, spa, 0, 0, w, (uint32_t*)b_pix.p,
-                                   (double*)b_dx.p, (double*)b_dy.p, st));
-  grt::WorkList wo;
-  std::memset(&wo, 0, sizeof(wo));
-  wo.rows = frame_rows;
-  wo.cols = w;
-  wo.n_items = ns;
-  wo.pixel_index = (const uint32_t*)b_pix.p;
-  wo.dx = (const double*)b_dx.p;
-  wo.dy = (const double*)b_dy.p;
-  grt::Outputs so{(float*)s_xyza.p, (uint8_t*)s_cls.p, (uint8_t*)s_status.p, (double*)s_x64.p, nullptr, nullptr};
-  if ((rc = enqueue_trace(s, *dc, wo, so, (unsigned long long*)d_stats, st))) return rc;
-  HIP_TRY(grt::launch_average((const uint32_t*)b_sel_local.p, n_sel, spa, (const double*)s_x64.p,
-                              (const uint8_t*)s_status.p, d_xyza64, st));
-  HIP_TRY(hipStreamSynchronize(st));  // the scratch buffers are freed on return
+  size_t bytes = 0;
+  HIP_TRY(grt::luminance_floor_device(d_y, stride, n, floor_index(n), nullptr, &bytes, nullptr, st));
+  if ((rc = ad_reserve(*dc, bytes))) return rc;
+  HIP_TRY(grt::luminance_floor_device(d_y, stride, n, floor_index(n), dc->ad_mem, &bytes, d_min_lum, st));
   return 0;
 }
 

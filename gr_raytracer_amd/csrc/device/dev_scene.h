@@ -107,6 +107,9 @@ struct WorkList {
   const double* dx;
   const double* dy;
   const uint32_t* tile_order;   // rectangle mode: queue position -> tile (NULL = row-major)
+  // offsets mode, count decided on the device (the adaptive pass): the items actually
+  // present are min(*n_live, n_items); n_items is the launch's capacity (NULL = n_items)
+  const unsigned long long* n_live;
 };
 
 // Hand-off from the integrate kernel to the shade kernel, structure-of-arrays with
@@ -131,6 +134,9 @@ struct Workspace {
   uint64_t* jobs;     // [MAX * n] raymarch jobs: (ray << 8) | candidate slot
   unsigned long long* march;  // [0] job count, [1] job cursor, [2] samples, [3] jobs (cumulative),
                               // [4] samples that evaluated the noise, [5] samples that emitted
+  // rays present when the count is decided on the device: min(*n_live, n) (NULL = n);
+  // n stays the SoA stride
+  const unsigned long long* n_live;
 };
 
 // Local row -> frame row under cyclic row-band sharding: band k of shard s is frame

@@ -1062,6 +1062,8 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr uint64_t CHUNK = 64;
   const uint64_t n = ws.n;
+  // items present: the capacity, or the count the adaptive pass decided on the device
+  const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
 
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
@@ -1092,7 +1094,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
       if (need) {
         uint64_t rank = __popcll(need_mask & lanemask_lt);
         uint64_t item = rank < remaining ? chunk_next + rank : new_base + (rank - remaining);
-        if (item >= wl.n_items) {
+        if (item >= n_items) {
           done = true;
         } else {
           double row, col;
@@ -1553,9 +1555,10 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
   const DevScene& S = *Sp;
   glibc::tables_to_lds();  // whole block, before the early return
   const uint64_t n = ws.n;
+  const uint64_t n_live = ws.n_live ? (uint64_t)min((unsigned long long)n, *ws.n_live) : n;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if constexpr (MODE == 1) {
-    const uint32_t mask = idx < n ? march_slots<G>(S, ws, idx) : 0u;
+    const uint32_t mask = idx < n_live ? march_slots<G>(S, ws, idx) : 0u;
     const int lane = threadIdx.x & 63;
     const uint32_t c = __popc(mask);
     uint32_t incl = c;  // inclusive wave prefix sum of the job counts
@@ -1572,7 +1575,7 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     for (uint32_t m = mask; m; m &= m - 1u) ws.jobs[pos++] = (idx << 8) | (uint64_t)__ffs(m) - 1u;
     return;
   }
-  if (idx >= n) return;
+  if (idx >= n_live) return;
   int status = ws.status[idx];
   int stop = ws.stop[idx];
   uint32_t steps = ws.steps[idx];

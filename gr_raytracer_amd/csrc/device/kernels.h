@@ -47,21 +47,46 @@ struct AdaptiveParams {
   double luminance_contrast_threshold;
   double opacity_contrast_threshold;
 };
+// d_min_lum (nullable): the luminance floor on the device, else p.min_lum.
 hipError_t launch_select(const double* d_xyza64, const uint8_t* d_cls, const AdaptiveParams& p,
-                         uint8_t* d_flags, hipStream_t stream);
+                         const double* d_min_lum, uint8_t* d_flags, hipStream_t stream);
 // The index-th of n luminances d_y[stride * i] in f64::total_cmp order, on the device
-// (radix sort).  Call with d_mem == NULL for the scratch size.
+// (radix sort; n <= INT_MAX).  Call with d_mem == NULL for the scratch size.
+// luminance_order_stat returns the value to the host; luminance_floor_device writes
+// 1e-3 x the value (resolve_minimum_luminance) to *d_min_lum without a host copy.
 hipError_t luminance_order_stat(const double* d_y, uint32_t stride, uint64_t n, uint64_t index, void* d_mem,
                                 size_t* mem_bytes, double* value, hipStream_t stream);
-hipError_t launch_select_shard(const double* d_ya, const uint8_t* d_cls, const AdaptiveParams& p, uint32_t band_rows,
-                               uint32_t shard, uint32_t n_shards, uint32_t local_rows, uint8_t* d_flags,
-                               hipStream_t stream);
-hipError_t launch_make_offsets(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, uint32_t row0,
-                               uint32_t col0, uint32_t w, uint32_t* d_pix, double* d_dx, double* d_dy,
-                               hipStream_t stream);
-hipError_t launch_average(const uint32_t* d_sel, uint64_t n_sel, uint32_t spa, const double* d_samples,
-                          const uint8_t* d_status, double* d_out, hipStream_t stream);
-hipError_t launch_paint(const uint32_t* d_sel, uint64_t n_sel, const double* mask, double* d_out,
-                        hipStream_t stream);
+hipError_t luminance_floor_device(const double* d_y, uint32_t stride, uint64_t n, uint64_t index, void* d_mem,
+                                  size_t* mem_bytes, double* d_min_lum, hipStream_t stream);
+// Indices i < n with d_flags[i] != 0, in order, and their count (n <= INT_MAX).
+// Call with d_temp == NULL for *temp_bytes.
+hipError_t compact_flags(const uint8_t* d_flags, uint64_t n, uint32_t* d_out, unsigned long long* d_count, void* d_temp,
+                         size_t* temp_bytes, hipStream_t stream);
+hipError_t launch_select_shard(const double* d_ya, const uint8_t* d_cls, const AdaptiveParams& p,
+                               const double* d_min_lum, uint32_t band_rows, uint32_t shard, uint32_t n_shards,
+                               uint32_t local_rows, uint8_t* d_flags, hipStream_t stream);
+// The supersample helpers take a chunk of the selected list: n_sel entries starting at
+// position `base` of a list of *d_count entries (d_count NULL: all n_sel present).
+hipError_t launch_make_offsets(const uint32_t* d_sel, uint64_t n_sel, const unsigned long long* d_count, uint64_t base,
+                               uint32_t spa, uint32_t row0, uint32_t col0, uint32_t w, uint32_t* d_pix, double* d_dx,
+                               double* d_dy, hipStream_t stream);
+// Failed sub-samples of the supersample pass (device side; count NULL: not recorded).
+struct SubsampleFailures {
+  unsigned long long* count;
+  uint64_t* key;      // pixel * spa^2 + stratum
+  uint8_t* status;
+  uint64_t cap;
+};
+hipError_t launch_average(const uint32_t* d_sel_out, const uint32_t* d_sel_px, uint64_t n_sel,
+                          const unsigned long long* d_count, uint64_t base, uint32_t spa, const double* d_samples,
+                          const uint8_t* d_status, double* d_out, const SubsampleFailures& f, hipStream_t stream);
+hipError_t launch_paint(const uint32_t* d_sel, uint64_t n_sel, const unsigned long long* d_count, const double* mask,
+                        double* d_out, hipStream_t stream);
+// live[c] = sub-rays of chunk c (P selected pixels per chunk, `per` sub-rays each)
+hipError_t launch_chunk_live(const unsigned long long* d_count, uint32_t n_chunks, uint64_t P, uint32_t per,
+                             unsigned long long* d_live, hipStream_t stream);
+hipError_t launch_frame_index(const uint32_t* d_sel_local, const unsigned long long* d_count, uint64_t n_max, uint32_t w,
+                              uint32_t band_rows, uint32_t shard, uint32_t n_shards, uint32_t* d_sel_frame,
+                              hipStream_t stream);
 
 }  // namespace grt

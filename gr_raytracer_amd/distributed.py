@@ -254,7 +254,7 @@ def unpack_section_records(rec):
 
 def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int = 16, device: int = 0,
                           stream=None, dst: int = 0, group=None, stats=None, sampling_mask_xyza=None,
-                          tone_mapping=None, exposure: float = 1.0):
+                          tone_mapping=None, exposure: float = 1.0, failures=None, report=None):
     """render_section_to_cie_buffer (raytracer.rs:177-318) for a whole frame across
     `world` GPUs, with the reference's adaptive supersampling:
 
@@ -262,12 +262,18 @@ def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int
     2. ONE allgather of every pixel's (Y, alpha, class), 17 B per pixel: the selection
        stencil reads 8 neighbours, which may sit in another rank's bands, and the
        luminance floor is the 99th percentile of the whole frame;
-    3. every rank computes the same exact floor (grt_adaptive_min_luminance);
-    4. each rank selects and supersamples its own pixels (grt_supersample_shard);
+    3. every rank computes the same exact floor on its GPU (grt_adaptive_floor_device),
+       which stays in device memory;
+    4. each rank selects and supersamples its own pixels (grt_supersample_shard_device:
+       selection, compaction, chunked sub-ray traces, all sized on the device);
     5. ONE gather to `dst`: f64 XYZA + class + status (34 B per pixel), or, with
        `tone_mapping` (0 Reinhard, 1 GlobalLinear), the per-rank tone-mapped sRGB8 rows
        (3 B per pixel; GlobalLinear allreduces the channel maxima first).
 
+    failures: optional _lib.SubsampleFailures filled with this rank's failed sub-samples
+    (frame pixel indices; the reference logs them, raytracer.rs:357-362).  report:
+    optional dict that receives this rank's 1-spp "status" (device u8, local rows) and
+    the local rows' "frame_rows" (the errors the reference logs at raytracer.rs:232-239).
     cfg: grt_adaptive_config (default: the scene's own).  `enabled` false and no mask:
     plain 1-spp frame (render_section_to_cie_buffer_raw).  Returns on dst
     (xyza64 (n,4) f64, class u8, status u8, n_supersampled over all ranks) or, with
@@ -297,27 +303,33 @@ def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int
     L.check(lib.grt_render_shard_async(scene._s, device, stream.cuda_stream, C.byref(sh), xyza.data_ptr(),
                                        cls.data_ptr(), status.data_ptr(), xyza64.data_ptr(), None, None,
                                        stats.data_ptr()), "grt_render_shard_async")
+    if report is not None:
+        report["status"] = status
+        report["frame_rows"] = shard_frame_rows(rows, band_rows, rank, world)
     n_sel = torch.zeros(1, dtype=torch.int64)
     with torch.cuda.stream(stream):
         if cfg.enabled or sampling_mask_xyza is not None:
             frame = allgather_frame(pack_luminance_records(xyza64, cls), rows, cols, band_rows, rank, world, group)
             frame_ya, frame_cls = unpack_luminance_records(frame)
-            # the frame's exact 99th-percentile floor, selected on this GPU (no host copy)
-            floor = C.c_double(0.0)
-            L.check(lib.grt_adaptive_min_luminance_device(device, stream.cuda_stream, frame_ya.data_ptr(), 2,
-                                                          frame_ya.shape[0], C.byref(cfg), C.byref(floor)),
-                    "grt_adaptive_min_luminance_device")
-            min_lum = floor.value
+            # the frame's exact 99th-percentile floor, selected on this GPU and left there
+            # (a configured minimum_luminance is a constant)
+            d_floor = None
+            if not cfg.has_minimum_luminance:
+                d_floor = torch.empty(1, dtype=torch.float64, device=dev)
+                L.check(lib.grt_adaptive_floor_device(scene._s, device, stream.cuda_stream, frame_ya.data_ptr(), 2,
+                                                      frame_ya.shape[0], d_floor.data_ptr()),
+                        "grt_adaptive_floor_device")
             mask = None
             if sampling_mask_xyza is not None:
                 mask = (C.c_double * 4)(*[float(v) for v in sampling_mask_xyza])
-            count = C.c_uint64(0)
-            L.check(lib.grt_supersample_shard(scene._s, device, stream.cuda_stream, C.byref(sh), C.byref(cfg),
-                                              min_lum, frame_ya.data_ptr(), frame_cls.data_ptr(), mask,
-                                              xyza64.data_ptr(), C.byref(count), stats.data_ptr()),
-                    "grt_supersample_shard")
-            total = torch.tensor([count.value], dtype=torch.int64, device=dev)
-            total = total.to(_collective_device(total, group))
+            count = torch.zeros(1, dtype=torch.int64, device=dev)
+            L.check(lib.grt_supersample_shard_device(scene._s, device, stream.cuda_stream, C.byref(sh), C.byref(cfg),
+                                                     float(cfg.minimum_luminance),
+                                                     d_floor.data_ptr() if d_floor is not None else None,
+                                                     frame_ya.data_ptr(), frame_cls.data_ptr(), mask,
+                                                     xyza64.data_ptr(), count.data_ptr(), stats.data_ptr(), failures),
+                    "grt_supersample_shard_device")
+            total = count.to(_collective_device(count, group))
             dist.all_reduce(total, op=dist.ReduceOp.SUM, group=group)
             n_sel[0] = int(total[0])
         if tone_mapping is not None:

@@ -25,6 +25,11 @@ import time
 RENDER_FLAGS = ("--filename", "--from-row", "--from-col", "--to-row", "--to-col")
 
 
+# Debug names of the RaytracerError variants a pixel can end in (grt_main.cpp's table)
+ERROR_NAMES = {1: "IntegrationError(MaxStepsReached)", 2: "NoCircularOrbitPossible", 3: "BelowRISCO",
+               4: "NonFiniteRadius"}
+
+
 def _csv(n: int, conv=float):
     def parse(v: str):
         parts = v.split(",")
@@ -124,10 +129,26 @@ def main(argv=None) -> int:
         stats = torch.zeros(4, dtype=torch.int64, device=torch.device("cuda", device))
         dist.barrier()
         t0 = time.perf_counter()
+        fail_cap = 1 << 20
+        f_pix, f_smp, f_st = np.zeros(fail_cap, np.uint32), np.zeros(fail_cap, np.uint32), np.zeros(fail_cap, np.uint8)
+        fails = L.SubsampleFailures(fail_cap, L.ptr(f_pix, C.c_uint32), L.ptr(f_smp, C.c_uint32),
+                                    L.ptr(f_st, C.c_uint8), 0)
+        report = {}
         out = render_frame_adaptive(scene, rank, world, band_rows=a.band_rows, device=device, stats=stats,
-                                    sampling_mask_xyza=mask, tone_mapping=None if want_f64 else tone)
+                                    sampling_mask_xyza=mask, tone_mapping=None if want_f64 else tone,
+                                    failures=C.byref(fails), report=report)
         torch.cuda.synchronize()
         t_render = time.perf_counter() - t0
+        # raytracer.rs:232-239 and :357-362: each rank logs its own pixels' failures
+        st_local = report["status"].cpu().numpy().reshape(-1, scene.cols)
+        for li, fi in zip(*np.nonzero(st_local & 0x7F)):
+            print(f"[render_dist] ERROR Unable to compute color for ray at pixel ({fi}, "
+                  f"{report['frame_rows'][li]}): {ERROR_NAMES.get(int(st_local[li, fi] & 0x7F), 'Unknown')}",
+                  file=sys.stderr)
+        for k in range(min(int(fails.count), fail_cap)):
+            row, col = divmod(int(f_pix[k]), scene.cols)
+            print(f"[render_dist] ERROR Unable to compute color for ray at pixel ({col}, {row}): "
+                  f"{ERROR_NAMES.get(int(f_st[k]), 'Unknown')}", file=sys.stderr)
         if dist.get_backend() == "gloo":
             host = stats.cpu()
             dist.all_reduce(host)

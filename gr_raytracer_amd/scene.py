@@ -118,6 +118,17 @@ class RenderResult:
     stats: dict = field(default_factory=dict)
 
 
+@dataclass
+class SectionResult:
+    xyza64: np.ndarray          # float64 (n, 4)
+    ray_class: np.ndarray       # uint8 (n,)
+    status: np.ndarray          # uint8 (n,): the 1-spp ray's status
+    n_supersampled: int
+    stats: dict
+    n_failed_subsamples: int
+    failed_subsamples: np.ndarray  # (m, 3) uint32: section pixel, stratum, status (m <= capacity)
+
+
 def _stats_dict(st: L.Stats) -> dict:
     return {"accepted_steps": int(st.accepted_steps), "attempts": int(st.attempts), "rays": int(st.rays),
             "hit_overflows": int(st.hit_overflows), "kernel_ms": float(st.kernel_ms),
@@ -208,23 +219,41 @@ class Scene:
     def render_section(self, from_row: int = 0, from_col: int = 0, to_row: Optional[int] = None,
                        to_col: Optional[int] = None, adaptive: Optional[L.AdaptiveConfig] = None,
                        sampling_mask_xyza=None, device: int = 0):
-        """render_section_to_cie_buffer (raytracer.rs:177-318): f64 XYZA per pixel."""
+        """render_section_to_cie_buffer (raytracer.rs:177-318): f64 XYZA per pixel.
+        Returns (xyza64, class, n_supersampled, stats)."""
+        r = self.render_section_ex(from_row, from_col, to_row, to_col, adaptive, sampling_mask_xyza, device)
+        return r.xyza64, r.ray_class, r.n_supersampled, r.stats
+
+    def render_section_ex(self, from_row: int = 0, from_col: int = 0, to_row: Optional[int] = None,
+                          to_col: Optional[int] = None, adaptive: Optional[L.AdaptiveConfig] = None,
+                          sampling_mask_xyza=None, device: int = 0, failure_capacity: int = 1 << 16):
+        """render_section plus each pixel's 1-spp status and the failed supersample
+        sub-rays ((pixel, stratum, status), sorted; raytracer.rs:232-239, :357-362)."""
         to_row = self.rows if to_row is None else to_row
         to_col = self.cols if to_col is None else to_col
         n = (to_row - from_row) * (to_col - from_col)
         out = np.zeros((n, 4), np.float64)
         cls = np.zeros(n, np.uint8)
+        status = np.zeros(n, np.uint8)
         nsel = C.c_uint64(0)
         st = L.Stats()
         mask = None
         if sampling_mask_xyza is not None:
             mask = np.ascontiguousarray(sampling_mask_xyza, np.float64)
-        L.check(L.lib().grt_render_section(self._s, device, from_row, from_col, to_row, to_col,
-                                           C.byref(adaptive or self.adaptive),
-                                           L.dptr(mask) if mask is not None else None, L.dptr(out),
-                                           L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st), None),
-                "grt_render_section")
-        return out, cls, int(nsel.value), _stats_dict(st)
+        fp = np.zeros(failure_capacity, np.uint32)
+        fs = np.zeros(failure_capacity, np.uint32)
+        fst = np.zeros(failure_capacity, np.uint8)
+        fails = L.SubsampleFailures(failure_capacity, L.ptr(fp, C.c_uint32), L.ptr(fs, C.c_uint32),
+                                    L.ptr(fst, C.c_uint8), 0)
+        L.check(L.lib().grt_render_section_ex(self._s, device, from_row, from_col, to_row, to_col,
+                                              C.byref(adaptive or self.adaptive),
+                                              L.dptr(mask) if mask is not None else None, L.dptr(out),
+                                              L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st),
+                                              L.ptr(status, C.c_uint8), C.byref(fails)),
+                "grt_render_section_ex")
+        m = min(int(fails.count), failure_capacity)
+        return SectionResult(out, cls, status, int(nsel.value), _stats_dict(st), int(fails.count),
+                             np.stack([fp[:m], fs[:m], fst[:m].astype(np.uint32)], axis=1))
 
     def _trace(self, fn, a, b, width: int, capacity: int, device: int):
         a = np.ascontiguousarray(a, np.float64).reshape(-1, width)

@@ -363,6 +363,28 @@ int grt_render_section(grt_scene* scene, int device, uint32_t from_row, uint32_t
                        uint8_t* status_out /* nullable: grt_status of each pixel's 1-spp ray, the
                                               error the reference logs at raytracer.rs:232-239 */);
 
+/* Failed sub-samples of the supersample pass (supersample's Err arm, raytracer.rs:357-362,
+ * which the reference logs as "Unable to compute color for ray at pixel (col, row)").
+ * The caller provides `capacity` entries; `count` returns how many failed (it may exceed
+ * the capacity).  Entries are sorted by (pixel, sample). */
+typedef struct grt_subsample_failures {
+  uint64_t capacity;
+  uint32_t* pixel;   /* pixel index, row-major in the section (shard: in the frame)      */
+  uint32_t* sample;  /* nullable: stratum index stratum_row * spa + stratum_col          */
+  uint8_t* status;   /* grt_status of the failed sub-sample ray                         */
+  uint64_t count;    /* out                                                             */
+} grt_subsample_failures;
+
+/* grt_render_section plus the failed sub-samples (nullable).  The whole section stays
+ * on the device between the 1-spp pass and the supersample pass: the luminance floor,
+ * the selection, its compaction and count, and the sub-ray launches' sizes are decided
+ * there (no host round trip). */
+int grt_render_section_ex(grt_scene* scene, int device, uint32_t from_row, uint32_t from_col,
+                          uint32_t to_row, uint32_t to_col, const grt_adaptive_config* cfg,
+                          const double* sampling_mask_xyza, double* xyza_out, uint8_t* class_out,
+                          uint64_t* n_supersampled, grt_stats* stats, uint8_t* status_out,
+                          grt_subsample_failures* failures);
+
 /* Row-band sharding of one frame across GPUs (multi-GPU render).
  * The frame's rows are cut into bands of `band_rows` rows (the last may be short);
  * shard s of n owns the bands b with b % n == s.  Its output is the full-width rows of
@@ -423,6 +445,22 @@ int grt_supersample_shard(grt_scene* scene, int device, void* stream, const grt_
                           const grt_adaptive_config* cfg, double min_lum, const double* d_frame_ya,
                           const uint8_t* d_frame_class, const double* sampling_mask_xyza,
                           double* d_xyza64, uint64_t* n_supersampled, uint64_t* d_stats);
+/* The same, asynchronous on `stream` with everything on the device: the floor is
+ * *d_min_lum when d_min_lum is non-null (grt_adaptive_floor_device), else min_lum; the
+ * selection count goes to *d_n_supersampled (device uint64, nullable).  failures
+ * (nullable) synchronises `stream` to return the failed sub-samples (frame pixel
+ * indices). */
+int grt_supersample_shard_device(grt_scene* scene, int device, void* stream, const grt_row_shard* sh,
+                                 const grt_adaptive_config* cfg, double min_lum, const double* d_min_lum,
+                                 const double* d_frame_ya, const uint8_t* d_frame_class,
+                                 const double* sampling_mask_xyza, double* d_xyza64,
+                                 uint64_t* d_n_supersampled, uint64_t* d_stats,
+                                 grt_subsample_failures* failures);
+/* resolve_minimum_luminance's relative floor of n DEVICE luminances d_y[stride * i],
+ * written to *d_min_lum (device double) on `stream` without a host copy (n <= INT_MAX;
+ * n = 0 gives +0.0).  A configured minimum_luminance is the caller's constant instead. */
+int grt_adaptive_floor_device(grt_scene* scene, int device, void* stream, const double* d_y, uint32_t stride,
+                              uint64_t n, double* d_min_lum);
 
 /* The image files of Raytracer::render_section (raytracer.rs:460-497): an 8-bit RGB
  * PNG, and the Radiance .hdr that stores XYZ as its RGB channels (f32, RGBE). */

@@ -187,3 +187,56 @@ def test_c5_adaptive_full_frame(grt, oracle, gpu):
         assert np.all(np.abs(out[p] - want) <= 1e-4 * np.maximum(np.abs(want), 1e-6)), (p, out[p], want)
         n_checked += 1
     assert n_checked >= 240
+
+
+def test_failed_subsamples_are_reported(grt, oracle, gpu):
+    """supersample's Err arm (raytracer.rs:357-362): every failed sub-sample ray is
+    reported with its pixel, stratum and error, as the oracle's sub-rays say."""
+    import ctypes as C
+    import math
+
+    b = grt.SceneBuilder(1, radius=2.0, horizon_epsilon=1e-4)
+    b.integration(20000, 100.0, 0.01, 1e-7)
+    pos = grt.cartesian_to_spherical((0.0, -16.0, 0.0, 3.5))
+    vel = grt.stationary_velocity(1, 2.0, 0.0, pos)
+    b.camera(pos, vel, math.pi / 4, 48, 48, 0.0, -3.142, 0.0)
+    b.celestial(grt.Checker(0.0, 20.0, 20.0, (0, 255, 0), (0, 100, 0)))
+    b.add_disc(3.0, 12.0, grt.BlackBody(1.0), temperature=5000.0)  # reaches inside the ISCO: BelowRISCO
+    d = b.build()
+    sc = grt.Scene(C.pointer(d), keepalive=(d, b))
+    ad = grt.scene.default_adaptive()
+    ad.enabled, ad.samples_per_axis = 1, 4
+    mark = np.array([-1.0, -2.0, -3.0, -4.0])
+    painted = sc.render_section_ex(adaptive=ad, sampling_mask_xyza=mark)
+    sel = np.flatnonzero(np.all(painted.xyza64 == mark, axis=1))
+    r = sc.render_section_ex(adaptive=ad)
+    assert r.n_supersampled == sel.size > 0
+    assert np.array_equal(r.status, painted.status)  # the 1-spp statuses
+    # the oracle's sub-rays of every selected pixel, in (pixel, stratum) order
+    R, Cc, DX, DY, KEY = [], [], [], [], []
+    for p in sel:
+        row, col = divmod(int(p), 48)
+        for s in range(16):
+            dx, dy = oracle.stratified_offset(row, col, s // 4, s % 4, 4)
+            R.append(row); Cc.append(col); DX.append(dx); DY.append(dy); KEY.append(int(p) * 16 + s)
+    R, Cc, DX, DY, KEY = map(np.asarray, (R, Cc, DX, DY, KEY))
+    ref = oracle_pixels(oracle, d, 48, R, Cc, DX, DY)
+    want = {(int(k) // 16, int(k) % 16): int(st) for k, st in zip(KEY, ref["status"]) if st != 0}
+    got = {(int(p), int(s)): int(st) for p, s, st in r.failed_subsamples}
+    assert r.n_failed_subsamples == len(r.failed_subsamples)
+    assert len(want) > 10  # the scene does fail sub-rays
+    # sorted by (pixel, stratum)
+    keys = [p * 16 + s for p, s, _ in r.failed_subsamples]
+    assert keys == sorted(keys)
+    diff = sorted(set(want.items()) ^ set(got.items()))
+    if diff:  # only libm-sensitive sub-rays may differ
+        idx = np.array([int(np.flatnonzero(KEY == p * 16 + s)[0]) for (p, s), _ in diff])
+        moved = np.zeros(idx.size, bool)
+        try:
+            for mode in PROBES:
+                oracle.lib().oracle_set_libm_perturbation(mode)
+                pr = oracle_pixels(oracle, d, 48, R[idx], Cc[idx], DX[idx], DY[idx])
+                moved |= pr["status"] != ref["status"][idx]
+        finally:
+            oracle.lib().oracle_set_libm_perturbation(0)
+        assert moved.all(), diff
