@@ -258,7 +258,25 @@ def test_grt_cli_logs_failed_pixels_like_the_reference(grt, oracle, gpu, tmp_pat
     ref = oracle.render_pixels(hs.desc, 0, 0, 64, 64, threads=16)
     st = ref["status"].reshape(64, 64) & 0x7F
     want = {(int(c), int(rw), names[int(st[rw, c])]) for rw, c in zip(*np.nonzero(st))}
-    assert len(want) > 10 and got == want
+    assert len(want) > 10
+    # the stock TOML supersamples: supersample's Err arm (raytracer.rs:357-362) logs every
+    # failed sub-ray of a selected pixel with the same message
+    ad = hs.adaptive
+    assert ad.enabled
+    sel, _ = oracle.select_pixels(ref["xyza"], ref["ray_class"], 64, 64, ad)
+    spa = ad.samples_per_axis
+    pix, dx, dy = [], [], []
+    for p in np.flatnonzero(sel):
+        row, col = divmod(int(p), 64)
+        for s in range(spa * spa):
+            ox, oy = oracle.stratified_offset(row, col, s // spa, s % spa, spa)
+            pix.append(p); dx.append(ox); dy.append(oy)
+    sub = oracle.render_pixels(hs.desc, 0, 0, 64, 64, threads=16,
+                               offsets=(np.asarray(pix), np.asarray(dx), np.asarray(dy)))
+    for p, s in zip(pix, sub["status"] & 0x7F):
+        if s:
+            want.add((int(p) % 64, int(p) // 64, names[int(s)]))
+    assert got == want
 
 
 @pytest.mark.gpu
