@@ -27,6 +27,7 @@ namespace {
 int g_blocks_per_cu = 0;
 int g_threads = 256;
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
+long long g_tail = -1;  // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
 constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
 
 
@@ -37,8 +38,10 @@ int fail(int code, const std::string& msg) {
 #define HIP_TRY(expr)                                                                    \
   do {                                                                                   \
     hipError_t _e = (expr);                                                              \
-    if (_e != hipSuccess)                                                                \
+    if (_e != hipSuccess) {                                                              \
+      (void)hipGetLastError(); /* clear it: a later launch check must not see it */    \
       return fail(-EIO, std::string(#expr) + ": " + hipGetErrorString(_e));             \
+    }                                                                                    \
   } while (0)
 
 struct HostTexture {
@@ -68,6 +71,10 @@ struct DeviceCopy {
   // grow-only: no allocation (and no implicit device synchronisation) between passes
   uint64_t ad_bytes = 0;
   void* ad_mem = nullptr;
+  // long-ray hand-off (Kerr-Schild): [0] live, [1] handed off, [2] claim cursor; entries, grow-only
+  unsigned long long* d_tail_ctl = nullptr;
+  uint64_t tail_cap = 0;
+  unsigned long long* tail_mem = nullptr;
 };
 
 // Carve a Workspace for n rays out of the device's grow-only arena.
@@ -85,6 +92,8 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
     dc.ws_mem = nullptr;
     uint64_t cap = std::max<uint64_t>(n, 1 << 16);
     if (hipMalloc(&dc.ws_mem, cap * per_ray + 32 * 256) != hipSuccess) {  // + per-array alignment
+      (void)hipGetLastError();
+      dc.ws_mem = nullptr;
       dc.ws_cap = 0;
       return fail(-ENOMEM, "cannot allocate the integrate/shade workspace");
     }
@@ -336,6 +345,10 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   dc.d_counter = (unsigned long long*)p;
   dc.d_stats = dc.d_counter + 1;
   dc.d_march = dc.d_counter + 8;
+  HIP_TRY(hipMalloc(&p, 4 * sizeof(unsigned long long)));
+  dc.allocations.push_back(p);
+  HIP_TRY(hipMemset(p, 0, 4 * sizeof(unsigned long long)));
+  dc.d_tail_ctl = (unsigned long long*)p;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   dc.cus = prop.multiProcessorCount;
@@ -425,6 +438,36 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   return 0;
 }
 
+// Long-ray hand-off of a Kerr-Schild trace (TailList, dev_scene.h): the tail kernel runs
+// one block of 4 waves per CU per GRT_TAIL_WAVES, 64 rays per block (a quad each); by
+// default the integrate kernel hands off once the queue is drained and no more rays are
+// live than the tail kernel integrates at once.  A lane holds at most one ray, so the
+// entry arena needs one entry per integrate lane whatever the threshold.
+int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList* tl, int* tail_blocks) {
+  std::memset(tl, 0, sizeof(*tl));
+  *tail_blocks = 0;
+  if (s->desc.geometry != GRT_GEOM_KERR || dc.vol || g_tail == 0) return 0;
+  const int blocks = dc.cus * GRT_TAIL_WAVES;
+  const uint64_t threshold = g_tail > 0 ? (uint64_t)g_tail : (uint64_t)blocks * grt::TAIL_RAYS_PER_BLOCK;
+  const uint64_t cap = lanes;
+  if (cap > dc.tail_cap) {
+    if (dc.tail_mem) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(dc.tail_mem);
+      dc.tail_mem = nullptr;
+    }
+    dc.tail_cap = 0;
+    HIP_TRY(hipMalloc(&dc.tail_mem, cap * 16 * sizeof(unsigned long long)));
+    dc.tail_cap = cap;
+  }
+  tl->ctl = dc.d_tail_ctl;
+  tl->cap = dc.tail_cap;
+  tl->threshold = threshold;
+  tl->st = dc.tail_mem;
+  *tail_blocks = blocks;
+  return 0;
+}
+
 // Enqueue one trace over `wl` on `stream`; counters are zeroed first.
 int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, const grt::Outputs& o,
                   unsigned long long* d_stats, hipStream_t stream) {
@@ -445,8 +488,13 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   int rc = ensure_workspace(dc, n_out, &ws);
   if (rc) return rc;
   ws.n_live = wl.n_live;
+  grt::TailList tl;
+  int tail_blocks = 0;
+  rc = tail_list(s, dc, blocks * (uint64_t)threads, &tl, &tail_blocks);
+  if (rc) return rc;
+  if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 4 * sizeof(unsigned long long), stream));
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
-                            dc.vol, stream));
+                            dc.vol, tl, tail_blocks, stream));
   return 0;
 }
 
@@ -512,6 +560,27 @@ int grt_set_launch_config(int blocks_per_cu, int threads_per_block) {
   return 0;
 }
 
+int grt_set_tail(long long threshold) {
+  if (threshold < -1) return fail(-EINVAL, "tail threshold must be -1 (auto), 0 (off) or a ray count");
+  g_tail = threshold;
+  return 0;
+}
+
+int grt_tail_handoffs(grt_scene* scene, int device, uint64_t* handed_off) {
+  if (!scene || !handed_off) return fail(-EINVAL, "null argument");
+  *handed_off = 0;
+  if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
+    return 0;
+  DeviceCopy& dc = *scene->devices[device];
+  std::lock_guard<std::mutex> lock(dc.mu);
+  HIP_TRY(hipSetDevice(device));
+  unsigned long long v[4];
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(v, dc.d_tail_ctl, sizeof(v), hipMemcpyDeviceToHost));
+  *handed_off = v[1];
+  return 0;
+}
+
 int grt_set_schedule(int mode) {
   if (mode < -1 || mode > 1) return fail(-EINVAL, "schedule mode must be -1 (auto), 0 or 1");
   g_schedule = mode;
@@ -560,6 +629,7 @@ int grt_scene_destroy(grt_scene* s) {
     if (dc->ws_mem) (void)hipFree(dc->ws_mem);
     if (dc->sched_mem) (void)hipFree(dc->sched_mem);
     if (dc->ad_mem) (void)hipFree(dc->ad_mem);
+    if (dc->tail_mem) (void)hipFree(dc->tail_mem);
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
     delete dc;
@@ -757,7 +827,11 @@ static int ad_reserve(DeviceCopy& dc, uint64_t bytes) {
     dc.ad_bytes = 0;
   }
   const uint64_t cap = bytes + (bytes >> 3);
-  if (hipMalloc(&dc.ad_mem, cap) != hipSuccess) return fail(-ENOMEM, "cannot allocate the adaptive-pass scratch");
+  if (hipMalloc(&dc.ad_mem, cap) != hipSuccess) {
+    (void)hipGetLastError();
+    dc.ad_mem = nullptr;
+    return fail(-ENOMEM, "cannot allocate the adaptive-pass scratch");
+  }
   dc.ad_bytes = cap;
   return 0;
 }

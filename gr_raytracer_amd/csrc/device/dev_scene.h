@@ -152,6 +152,24 @@ inline uint32_t shard_frame_row(uint32_t band_rows, uint32_t shard, uint32_t n_s
 #ifndef GRT_INTEGRATE_WAVES
 #define GRT_INTEGRATE_WAVES 2  // min waves per SIMD requested for the integrate kernel
 #endif
+#ifndef GRT_TAIL_WAVES
+#define GRT_TAIL_WAVES 1  // waves per SIMD of the tail kernel: a lone wave owns its SIMD's issue slots
+#endif
+
+// Long-ray hand-off (Kerr-Schild).  Once the tile queue is drained and at most
+// `threshold` rays are still being integrated, the integrate kernel's waves write their
+// rays' loop state here and exit; tail_kernel continues each ray on the 4 lanes of a
+// quad (the three acceleration components of the Kerr-Schild RHS in parallel), one
+// wave per SIMD.  The split changes who computes a value, never its operations, so every
+// result is identical to integrating the ray on one lane (tests/test_tail.py).
+struct TailList {
+  unsigned long long* ctl;  // [0] live rays (started - ended), [1] rays handed off, [2] tail claim cursor
+  uint64_t cap;             // entries of st (0: hand-off disabled)
+  uint64_t threshold;       // hand off once the queue is drained and live <= threshold
+  // [16][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,
+  // nrec | retries << 32 | c_valid << 48
+  unsigned long long* st;
+};
 
 struct Outputs {
   float* xyza;        // 4 floats per sample

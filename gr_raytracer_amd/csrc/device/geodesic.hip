@@ -383,6 +383,49 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
   }
 }
 
+// Lane K's value of v in every lane of its quad (DPP quad_perm [K,K,K,K], no LDS).
+template <int K>
+GDEV double quad_bcast(double v) {
+  constexpr int ctrl = K | (K << 2) | (K << 4) | (K << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// rhs<KERR> on the 4 lanes of a quad (tail_kernel): every lane forms the contravariant
+// metric and xdot as rhs<KERR> does; lane `sub` < 3 evaluates acceleration component
+// sub + 1 (lane 3 repeats component 3), and the three components are broadcast across
+// the quad.  Every value comes out of the same operations as in rhs<KERR>, so o is
+// bit-identical in all four lanes; the quad's lanes must be active together.
+GDEV void rhs_ks_quad(const DevScene& S, const double* y, double* o, int sub) {
+  const double radius = S.radius, a = S.a;
+  const double x = y[1], yy = y[2], z = y[3];
+  const double p[4] = {y[4], y[5], y[6], y[7]};
+  double Gc[4][4];
+  ks_metric_contra(radius, a, x, yy, z, Gc);
+  double xdot[4];
+  mat_vec(Gc, p, xdot);
+  const double acc = ks_accel(radius, a, sub < 3 ? sub + 1 : 3, x, yy, z, Gc, p);
+  o[0] = xdot[0];
+  o[1] = xdot[1];
+  o[2] = xdot[2];
+  o[3] = xdot[3];
+  o[4] = 0.0;
+  o[5] = quad_bcast<0>(acc);
+  o[6] = quad_bcast<1>(acc);
+  o[7] = quad_bcast<2>(acc);
+}
+
+template <int G, bool QUAD>
+GDEV void rhs_sel(const DevScene& S, const RayConst& rc, const double* y, double* o, int sub) {
+  if constexpr (QUAD) {
+    static_assert(G == GRT_GEOM_KERR, "the quad-split RHS is the Kerr-Schild one");
+    rhs_ks_quad(S, y, o, sub);
+  } else {
+    rhs<G>(S, rc, y, o);
+  }
+}
+
 // Number of state components that can be non-zero: KerrBL's y[6], y[7] are
 // identically 0 (its RHS returns literal zeros), so every RKF term on them is an
 // exact +-0 and the norm term a2 + a6 == a2; skipping them is bit-exact.
@@ -396,39 +439,40 @@ struct Dim {
 // UNIT_H: every lane of the wave has h == 1.0 (H_MAX, the far field), where h * o is o
 // itself (x * 1.0 == x for every finite and infinite x and keeps the sign of zero; a NaN
 // stays a NaN, which stops the ray either way), so the eight products per stage go.
-template <int G, bool UNIT_H = false>
+// QUAD: the Kerr-Schild RHS split over a quad (rhs_ks_quad), `sub` = lane & 3.
+template <int G, bool UNIT_H = false, bool QUAD = false>
 GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
-                        double* yn) {
+                        double* yn, int sub = 0) {
   constexpr int D = Dim<G>::D;
   double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
-  rhs<G>(S, rc, y, o);
+  rhs_sel<G, QUAD>(S, rc, y, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k1[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
   if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
-  rhs<G>(S, rc, tmp, o);
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k2[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * k1[i] + B32 * k2[i];
-  rhs<G>(S, rc, tmp, o);
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k3[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * k1[i] + B42 * k2[i] + B43 * k3[i];
-  rhs<G>(S, rc, tmp, o);
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k4[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * k1[i] + B52 * k2[i] + B53 * k3[i] + B54 * k4[i];
-  rhs<G>(S, rc, tmp, o);
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k5[i] = UNIT_H ? o[i] : h * o[i];
 #pragma unroll
   for (int i = 0; i < D; ++i)
     tmp[i] = y[i] + B61 * k1[i] + B62 * k2[i] + B63 * k3[i] + B64 * k4[i] + B65 * k5[i];
-  rhs<G>(S, rc, tmp, o);
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k6[i] = UNIT_H ? o[i] : h * o[i];
   double e[8];
@@ -1047,15 +1091,117 @@ GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, int stop
   ws.steps[idx] = steps;
 }
 
+// The window (y -> yn) of accepted step i against every object in config order
+// (objects.rs:81); a hit nearer than the current nearest (objects.rs:86-88) is recorded
+// as candidate nrec: its object, window index, hit point and the lerped momentum
+// (objects.rs:27-44).  `writer`: this lane stores the candidate (one lane of a quad in
+// tail_kernel; every lane computes the same decisions).  c / c_valid follow yn.
+template <int G, bool VOL>
+GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc, uint64_t idx, const double* y,
+                      const double* yn, double* c, bool& c_valid, uint64_t i, uint32_t& nrec, bool writer) {
+  const uint64_t n = ws.n;
+  if (!window_far<G, VOL>(S, y, yn)) {
+    if (!c_valid) to_cart<G>(S, y, c);
+    double cn[3];
+    to_cart<G>(S, yn, cn);
+    double shortest = 1.7976931348623157e308;
+    for (uint32_t k = 0; k < S.n_objects; ++k) {
+      const DevObject& o = S.obj[k];
+      double t, pt[3];
+      bool hit;
+      if (VOL && o.kind == GRT_OBJ_VOLUMETRIC_DISC) hit = vdisc_chord(o, c, cn, &t, pt);
+      else hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
+      if (!hit) continue;
+      double wx = pt[0], wy = pt[1], wz = pt[2];
+      if (o.kind == GRT_OBJ_SPHERE) {
+        wx = pt[0] + o.cx;
+        wy = pt[1] + o.cy;
+        wz = pt[2] + o.cz;
+      }
+      double dx = wx - c[0], dy = wy - c[1], dz = wz - c[2];
+      double distance = sqrt(dx * dx + dy * dy + dz * dz);
+      if (!(distance < shortest)) continue;
+      shortest = distance;
+      if (writer && nrec < GRT_MAX_HITS) {
+        double pa[4], pb[4];
+        momentum<G>(S, rc, y, pa);
+        momentum<G>(S, rc, yn, pb);
+        double sw = 1.0 - t;
+        const uint64_t slot = (uint64_t)nrec * n + idx;
+        ws.rec_win[slot] = (uint32_t)i;
+        ws.rec_obj[slot] = (uint8_t)k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
+        if constexpr (VOL) {  // chord direction for the raymarch (volumetric_disc.rs:576, :589-594)
+          ws.rec_dir[slot] = cn[0] - c[0];
+          ws.rec_dir[(uint64_t)GRT_MAX_HITS * n + slot] = cn[1] - c[1];
+          ws.rec_dir[(uint64_t)2 * GRT_MAX_HITS * n + slot] = cn[2] - c[2];
+        }
+      }
+      nrec++;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = cn[k];
+    c_valid = true;
+  } else {
+    c_valid = false;
+  }
+}
+
+// A ray's loop state at the top of integrate_kernel's loop, in entry e of the tail list.
+struct LoopState {
+  double y[8], c[3];
+  double h, h_cur;
+  uint64_t i, idx;
+  uint32_t nrec;
+  int retries;
+  bool c_valid;
+};
+GDEV void tail_save(const TailList& tl, uint64_t e, const LoopState& s) {
+  unsigned long long* w = tl.st + e;
+  const uint64_t m = tl.cap;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k * m] = (unsigned long long)__double_as_longlong(s.y[k]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) w[(8 + k) * m] = (unsigned long long)__double_as_longlong(s.c[k]);
+  w[11 * m] = (unsigned long long)__double_as_longlong(s.h);
+  w[12 * m] = (unsigned long long)__double_as_longlong(s.h_cur);
+  w[13 * m] = s.i;
+  w[14 * m] = s.idx;
+  w[15 * m] = (unsigned long long)s.nrec | ((unsigned long long)(uint32_t)s.retries << 32) |
+              ((unsigned long long)(s.c_valid ? 1 : 0) << 48);
+}
+GDEV void tail_load(const TailList& tl, uint64_t e, LoopState& s) {
+  const unsigned long long* w = tl.st + e;
+  const uint64_t m = tl.cap;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s.y[k] = __longlong_as_double((long long)w[k * m]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.c[k] = __longlong_as_double((long long)w[(8 + k) * m]);
+  s.h = __longlong_as_double((long long)w[11 * m]);
+  s.h_cur = __longlong_as_double((long long)w[12 * m]);
+  s.i = w[13 * m];
+  s.idx = w[14 * m];
+  const unsigned long long f = w[15 * m];
+  s.nrec = (uint32_t)f;
+  s.retries = (int)((f >> 32) & 0xffffu);
+  s.c_valid = ((f >> 48) & 1u) != 0;
+}
+GDEV unsigned long long load_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One lane integrates one ray at a time: RKF45 attempts, and after every accepted
 // step the chord test of window (previous step, step) against every object in config
-// order (objects.rs:81) and the stop test.  A window hit nearer than the current
-// nearest (objects.rs:86-88) is recorded as a candidate: its object, window index,
-// hit point and the lerped momentum (objects.rs:27-44).
+// order (objects.rs:81) and the stop test (window_pass, should_stop).
+// Kerr-Schild with tl.cap != 0: once the tile queue is drained and at most tl.threshold
+// rays are live, each wave hands its rays to tail_kernel (tail_save) and exits.
 template <int G, bool VOL>
 __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     const DevScene* __restrict__ Sp, WorkList wl, Workspace ws, unsigned long long* __restrict__ counter,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, TailList tl) {
   const DevScene& S = *Sp;
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
@@ -1064,9 +1210,13 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   const uint64_t n = ws.n;
   // items present: the capacity, or the count the adaptive pass decided on the device
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
+  constexpr bool TAIL = (G == GRT_GEOM_KERR) && !VOL;
+  const bool tail_on = TAIL && tl.cap != 0;
 
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
+  bool started = false, ended = false;  // since the last live-count update (tail_on)
+  uint32_t poll = 0;
   uint64_t idx = 0;      // output slot of the current ray
   double y[8];           // state
   double c[3];           // Cartesian position of the last accepted step (when c_valid)
@@ -1133,10 +1283,12 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
             retries = 0;
             nrec = 0;
             active = true;
+            started = true;
             n_rays++;
             if (S.max_steps <= 1) {  // `for i in 1..max_steps` never runs
               store_ray(ws, idx, y, GRT_STOP_NONE, GRT_OK, 0, 0);
               active = false;
+              ended = true;
             }
           }
         }
@@ -1146,6 +1298,46 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
         chunk_end = new_base + CHUNK;
       } else {
         chunk_next += cnt;
+      }
+    }
+    if constexpr (TAIL) {
+      if (tail_on) {
+        // live-ray count: one atomic per wave when rays started or ended
+        const uint64_t st_mask = __ballot(started), en_mask = __ballot(ended);
+        started = ended = false;
+        const long long d = (long long)__popcll(st_mask) - (long long)__popcll(en_mask);
+        if (d != 0 && lane == 0) atomicAdd(&tl.ctl[0], (unsigned long long)d);
+        // hand-off: queue drained (and nothing left in this wave's chunk), few rays left
+        if ((chunk_next >= chunk_end || chunk_next >= n_items) && ((++poll & 15u) == 0u) &&
+            load_agent(counter) >= n_items &&
+            (long long)load_agent(&tl.ctl[0]) <= (long long)tl.threshold) {
+          const uint64_t ev = __ballot(active);
+          if (ev) {
+            unsigned long long b = 0;
+            if (lane == 0) b = atomicAdd(&tl.ctl[1], (unsigned long long)__popcll(ev));
+            b = __shfl(b, 0);
+            if (active) {
+              const uint64_t e = b + __popcll(ev & lanemask_lt);
+              if (e < tl.cap) {
+                LoopState s;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s.y[k] = y[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) s.c[k] = c[k];
+                s.h = h;
+                s.h_cur = h_cur;
+                s.i = i;
+                s.idx = idx;
+                s.nrec = nrec;
+                s.retries = retries;
+                s.c_valid = c_valid;
+                tail_save(tl, e, s);
+                active = false;
+                done = true;
+              }
+            }
+          }
+        }
       }
     }
     if (__ballot(!done) == 0) break;
@@ -1166,6 +1358,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
       if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
         store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
         active = false;
+        ended = true;
       }
       continue;
     }
@@ -1174,55 +1367,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     h = h_next;
     i++;
     n_acc++;
-    if (!window_far<G, VOL>(S, y, yn)) {
-      if (!c_valid) to_cart<G>(S, y, c);
-      double cn[3];
-      to_cart<G>(S, yn, cn);
-      // window (y -> yn) against every object; record each new nearest candidate
-      double shortest = 1.7976931348623157e308;
-      for (uint32_t k = 0; k < S.n_objects; ++k) {
-        const DevObject& o = S.obj[k];
-        double t, pt[3];
-        bool hit;
-        if (VOL && o.kind == GRT_OBJ_VOLUMETRIC_DISC) hit = vdisc_chord(o, c, cn, &t, pt);
-        else hit = (o.kind == GRT_OBJ_DISC) ? disc_chord(o, c, cn, &t, pt) : sphere_chord(o, c, cn, &t, pt);
-        if (!hit) continue;
-        double wx = pt[0], wy = pt[1], wz = pt[2];
-        if (o.kind == GRT_OBJ_SPHERE) {
-          wx = pt[0] + o.cx;
-          wy = pt[1] + o.cy;
-          wz = pt[2] + o.cz;
-        }
-        double dx = wx - c[0], dy = wy - c[1], dz = wz - c[2];
-        double distance = sqrt(dx * dx + dy * dy + dz * dz);
-        if (!(distance < shortest)) continue;
-        shortest = distance;
-        if (nrec < GRT_MAX_HITS) {
-          double pa[4], pb[4];
-          momentum<G>(S, rc, y, pa);
-          momentum<G>(S, rc, yn, pb);
-          double sw = 1.0 - t;
-          const uint64_t slot = (uint64_t)nrec * n + idx;
-          ws.rec_win[slot] = (uint32_t)i;
-          ws.rec_obj[slot] = (uint8_t)k;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
-          if constexpr (VOL) {  // chord direction for the raymarch (volumetric_disc.rs:576, :589-594)
-            ws.rec_dir[slot] = cn[0] - c[0];
-            ws.rec_dir[(uint64_t)GRT_MAX_HITS * n + slot] = cn[1] - c[1];
-            ws.rec_dir[(uint64_t)2 * GRT_MAX_HITS * n + slot] = cn[2] - c[2];
-          }
-        }
-        nrec++;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) c[k] = cn[k];
-      c_valid = true;
-    } else {
-      c_valid = false;
-    }
+    window_pass<G, VOL>(S, ws, rc, idx, y, yn, c, c_valid, i, nrec, true);
 #pragma unroll
     for (int k = 0; k < 8; ++k) y[k] = yn[k];
 
@@ -1230,6 +1375,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     if (stop != GRT_STOP_NONE || i == S.max_steps - 1) {
       store_ray(ws, idx, y, stop, GRT_OK, nrec, (uint32_t)i);
       active = false;
+      ended = true;
       continue;
     }
     retries = 0;
@@ -1247,6 +1393,97 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     atomicAdd(stats + 0, (unsigned long long)n_acc);
     atomicAdd(stats + 1, (unsigned long long)n_att);
     atomicAdd(stats + 2, (unsigned long long)n_rays);
+  }
+}
+
+// ============================================================= tail kernel =======
+// The rays integrate_kernel handed off (Kerr-Schild): the 4 lanes of a quad carry one
+// ray, splitting each RHS evaluation (rhs_ks_quad), and repeat the rest of the loop of
+// integrate_kernel in lockstep (identical values in all four lanes; lane 0 of the quad
+// writes).  A quad claims the next handed-off ray when its ray ends.  With one wave per
+// SIMD a long ray no longer shares issue slots with another wave.
+template <int G, bool VOL>
+__global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScene* __restrict__ Sp, Workspace ws,
+                                                                   TailList tl,
+                                                                   unsigned long long* __restrict__ stats) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before any lookup
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & 3;
+  const bool writer = sub == 0;
+  const uint64_t below_quad = (lane < 4) ? 0ull : (~0ull >> (64 - (lane & ~3)));
+  const uint64_t n = ws.n;
+  const unsigned long long handed = load_agent(&tl.ctl[1]);
+  const uint64_t n_tail = handed < tl.cap ? handed : tl.cap;  // final: integrate_kernel has ended
+
+  bool active = false, done = false;
+  LoopState s;
+  RayConst rc;
+  uint64_t n_acc = 0, n_att = 0;
+
+  while (true) {
+    const bool need = !active && !done;  // uniform within a quad
+    const uint64_t leaders = __ballot(need && writer);
+    if (leaders) {
+      unsigned long long b = 0;
+      if (lane == 0) b = atomicAdd(&tl.ctl[2], (unsigned long long)__popcll(leaders));
+      b = __shfl(b, 0);
+      if (need) {
+        const uint64_t e = b + __popcll(leaders & below_quad);
+        if (e >= n_tail) {
+          done = true;
+        } else {
+          tail_load(tl, e, s);
+          rc.obs = ws.rc[0 * n + s.idx];
+          rc.e = ws.rc[1 * n + s.idx];
+          rc.lz = ws.rc[2 * n + s.idx];
+          rc.q = ws.rc[3 * n + s.idx];
+          rc.pt = 0.0;
+          rc.pphi = 0.0;
+          active = true;
+        }
+      }
+    }
+    if (__ballot(!done) == 0) break;
+    if (!active) continue;
+
+    double yn[8];
+    const double err_sq = rkf_attempt<G, false, true>(S, rc, s.y, s.h_cur, yn, sub);
+    n_att++;
+    double h_next;
+    const int ctl = step_control(S, err_sq, s.h_cur, s.retries, h_next);
+    if (ctl != STEP_ACCEPTED) {
+      if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
+        if (writer) store_ray(ws, s.idx, s.y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)s.i);
+        active = false;
+      }
+      continue;
+    }
+    s.h = h_next;
+    s.i++;
+    n_acc++;
+    window_pass<G, VOL>(S, ws, rc, s.idx, s.y, yn, s.c, s.c_valid, s.i, s.nrec, writer);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s.y[k] = yn[k];
+    const int stop = should_stop<G>(S, s.y, s.c, s.c_valid, s.i);
+    if (stop != GRT_STOP_NONE || s.i == S.max_steps - 1) {
+      if (writer) store_ray(ws, s.idx, s.y, stop, GRT_OK, s.nrec, (uint32_t)s.i);
+      active = false;
+      continue;
+    }
+    s.retries = 0;
+    s.h_cur = rclamp(s.h, H_MIN, H_MAX);
+  }
+
+  if (!writer) n_acc = n_att = 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    n_acc += __shfl_down(n_acc, off);
+    n_att += __shfl_down(n_att, off);
+  }
+  if (lane == 0) {
+    atomicAdd(stats + 0, (unsigned long long)n_acc);
+    atomicAdd(stats + 1, (unsigned long long)n_att);
   }
 }
 
@@ -1659,24 +1896,33 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
 }
 
 // ------------------------------------------------------------------ launch -------
-// Plain scenes: integrate -> shade.  Volumetric scenes: integrate -> gather raymarch
-// jobs -> march (persistent, lane refill) -> composite; ws.march must be zeroed.
+// Plain scenes: integrate [-> tail] -> shade.  Volumetric scenes: integrate -> gather
+// raymarch jobs -> march (persistent, lane refill) -> composite; ws.march must be zeroed.
 template <int G>
 static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
                            unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
-                           bool vol, hipStream_t stream) {
+                           bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream) {
   const unsigned nb = (unsigned)((ws.n + 255) / 256);
+  TailList tl = tl_in;
+  if (G != GRT_GEOM_KERR || vol || tail_blocks <= 0) tl.cap = 0;
   if (!vol) {
     hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
-                       d_counter, d_stats);
+                       d_counter, d_stats, tl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if constexpr (G == GRT_GEOM_KERR) {
+      if (tl.cap) {
+        hipLaunchKernelGGL((tail_kernel<G, false>), dim3(tail_blocks), dim3(256), 0, stream, d_scene, ws, tl,
+                           d_stats);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+      }
+    }
     hipLaunchKernelGGL((shade_kernel<G, 0>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
     return hipGetLastError();
   }
   if (!ws.rec_dir || !ws.vcol || !ws.jobs || !ws.march) return hipErrorInvalidValue;
   hipLaunchKernelGGL((integrate_kernel<G, true>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
-                     d_counter, d_stats);
+                     d_counter, d_stats, tl);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((shade_kernel<G, 1>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
@@ -1689,21 +1935,24 @@ static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Wo
 
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
-                        int threads, bool vol, hipStream_t stream) {
+                        int threads, bool vol, const TailList& tl, int tail_blocks, hipStream_t stream) {
   if (ws.n == 0) return hipSuccess;
   switch (geometry) {
     case GRT_GEOM_EUCLIDEAN:
-      return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, stream);
+      return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
+                                          tail_blocks, stream);
     case GRT_GEOM_SCHWARZSCHILD:
-      return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
-                                              stream);
+      return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
+                                              tail_blocks, stream);
     case GRT_GEOM_KERR:
-      return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, stream);
+      return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl, tail_blocks,
+                                     stream);
     case GRT_GEOM_KERR_BL:
-      return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, stream);
+      return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
+                                        tail_blocks, stream);
     case GRT_GEOM_EUCLIDEAN_SPHERICAL:
       return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
-                                                    stream);
+                                                    tl, tail_blocks, stream);
     default:
       return hipErrorInvalidValue;
   }

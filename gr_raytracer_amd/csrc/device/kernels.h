@@ -9,9 +9,15 @@ namespace grt {
 // integrate_kernel (persistent, lane refill) then shade_kernel, all on `stream`.  With
 // `vol` (the scene has VolumetricDiscs): integrate, job gathering, march_kernel and the
 // composite; the workspace then needs its volumetric arrays, ws.march zeroed.
+// `tl.cap` != 0 (Kerr-Schild without volumetric objects only): long rays are handed to
+// tail_kernel (launched between integrate and shade on `stream`, `tail_blocks` blocks of
+// 256 threads); tl.ctl must be zeroed.
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
-                        int blocks, int threads, bool vol, hipStream_t stream);
+                        int blocks, int threads, bool vol, const TailList& tl, int tail_blocks,
+                        hipStream_t stream);
+// Tail kernel's quad capacity per block (rays integrated at once).
+constexpr int TAIL_RAYS_PER_BLOCK = 256 / 4;
 
 // Work-order probe: steps of one ray per 8x8 tile of `wl` (rectangle mode), capped.
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,

@@ -282,6 +282,18 @@ class Scene:
         r = self.render_pixels(row, col, 1, 1, device=device)
         return r.xyza64[0], int(r.ray_class[0]), int(r.status[0])
 
+    def tail_handoffs(self, device: int = 0) -> int:
+        """Rays the last Kerr-Schild trace on `device` handed to the tail kernel."""
+        n = C.c_uint64()
+        L.check(L.lib().grt_tail_handoffs(self._s, device, C.byref(n)), "grt_tail_handoffs")
+        return n.value
+
+
+def set_tail(threshold: int = -1) -> None:
+    """Long-ray hand-off of Kerr-Schild traces (grt_set_tail): -1 auto, 0 off, > 0 the
+    live-ray threshold.  Scheduling only; results are identical in every mode."""
+    L.check(L.lib().grt_set_tail(int(threshold)), "grt_set_tail")
+
 
 # --------------------------------------------------------- programmatic scenes ----
 @dataclass

@@ -523,6 +523,15 @@ int grt_set_launch_config(int blocks_per_cu, int threads_per_block);
  * max_steps >= 262144 over >= 1024 tiles; KerrBL's Mino-time rays are all short).
  * Scheduling only: every pixel's result is identical in all modes. */
 int grt_set_schedule(int mode);
+/* Long-ray hand-off of Kerr-Schild traces: once the tile queue is drained and at most
+ * `threshold` rays are still integrating, they continue in a tail kernel that splits each
+ * RHS evaluation over 4 lanes (one wave per SIMD).  -1 = automatic (default: on, threshold
+ * = the rays the tail kernel integrates at once, 64 per CU); 0 = off; > 0 = explicit
+ * threshold.  Scheduling only: every pixel's result is identical in all modes. */
+int grt_set_tail(long long threshold);
+/* Rays the last Kerr-Schild trace on `device` handed to the tail kernel (synchronises the
+ * device; 0 before the first trace).  A diagnostic of the scheduling above. */
+int grt_tail_handoffs(grt_scene* scene, int device, uint64_t* handed_off);
 
 #ifdef __cplusplus
 }
