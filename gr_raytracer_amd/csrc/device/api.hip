@@ -345,9 +345,9 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   dc.d_counter = (unsigned long long*)p;
   dc.d_stats = dc.d_counter + 1;
   dc.d_march = dc.d_counter + 8;
-  HIP_TRY(hipMalloc(&p, 4 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
   dc.allocations.push_back(p);
-  HIP_TRY(hipMemset(p, 0, 4 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(p, 0, 8 * sizeof(unsigned long long)));
   dc.d_tail_ctl = (unsigned long long*)p;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -492,7 +492,7 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   int tail_blocks = 0;
   rc = tail_list(s, dc, blocks * (uint64_t)threads, &tl, &tail_blocks);
   if (rc) return rc;
-  if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 4 * sizeof(unsigned long long), stream));
+  if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 8 * sizeof(unsigned long long), stream));
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
                             dc.vol, tl, tail_blocks, stream));
   return 0;
@@ -567,17 +567,34 @@ int grt_set_tail(long long threshold) {
 }
 
 int grt_tail_handoffs(grt_scene* scene, int device, uint64_t* handed_off) {
+  return grt_tail_report(scene, device, handed_off, nullptr, nullptr, nullptr, 0);
+}
+
+int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double timeline_s[3], uint64_t* slot,
+                    uint64_t* step, uint64_t capacity) {
   if (!scene || !handed_off) return fail(-EINVAL, "null argument");
   *handed_off = 0;
+  if (timeline_s) timeline_s[0] = timeline_s[1] = timeline_s[2] = 0.0;
   if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
     return 0;
   DeviceCopy& dc = *scene->devices[device];
   std::lock_guard<std::mutex> lock(dc.mu);
   HIP_TRY(hipSetDevice(device));
-  unsigned long long v[4];
+  unsigned long long v[8];
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(v, dc.d_tail_ctl, sizeof(v), hipMemcpyDeviceToHost));
   *handed_off = v[1];
+  if (timeline_s) {  // s_memrealtime ticks at 100 MHz
+    auto since = [&](unsigned long long t) { return (t && v[3]) ? (double)(long long)(t - v[3]) * 1e-8 : 0.0; };
+    timeline_s[0] = since(v[4]);
+    timeline_s[1] = since(v[5]);
+    timeline_s[2] = since(v[6]);
+  }
+  const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(v[1], dc.tail_cap), capacity);
+  if (n && dc.tail_mem) {
+    if (slot) HIP_TRY(hipMemcpy(slot, dc.tail_mem + 14 * dc.tail_cap, n * 8, hipMemcpyDeviceToHost));
+    if (step) HIP_TRY(hipMemcpy(step, dc.tail_mem + 13 * dc.tail_cap, n * 8, hipMemcpyDeviceToHost));
+  }
   return 0;
 }
 

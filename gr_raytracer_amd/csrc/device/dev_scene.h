@@ -163,7 +163,10 @@ inline uint32_t shard_frame_row(uint32_t band_rows, uint32_t shard, uint32_t n_s
 // wave per SIMD.  The split changes who computes a value, never its operations, so every
 // result is identical to integrating the ray on one lane (tests/test_tail.py).
 struct TailList {
-  unsigned long long* ctl;  // [0] live rays (started - ended), [1] rays handed off, [2] tail claim cursor
+  // [0] live rays (started - ended), [1] rays handed off, [2] tail claim cursor; timeline
+  // (s_memrealtime, 100 MHz): [3] integrate start, [4] queue drained, [5] first hand-off,
+  // [6] tail kernel end
+  unsigned long long* ctl;
   uint64_t cap;             // entries of st (0: hand-off disabled)
   uint64_t threshold;       // hand off once the queue is drained and live <= threshold
   // [16][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,

@@ -43,6 +43,9 @@ namespace grt {
 #ifndef GRT_UNIT_H
 #define GRT_UNIT_H 1  // far-field attempts of a wave with h == 1 everywhere skip h * o
 #endif
+#ifndef GRT_KLDS_GEOMS
+#define GRT_KLDS_GEOMS (1 << GRT_GEOM_KERR)  // integrate kernels whose RKF stages k1..k4 live in LDS
+#endif
 
 // f64::powf == glibc pow: bit-exact on glibc's fast path, OCML outside it.
 GDEV double rpow(double x, double y) {
@@ -439,48 +442,91 @@ struct Dim {
 // UNIT_H: every lane of the wave has h == 1.0 (H_MAX, the far field), where h * o is o
 // itself (x * 1.0 == x for every finite and infinite x and keeps the sign of zero; a NaN
 // stays a NaN, which stops the ray either way), so the eight products per stage go.
+// Stage values k1..k4 parked in LDS (KLDS): slot j of component i of thread t at
+// kl_buf[(j * 8 + i) * KL_STRIDE + t].  The Kerr-Schild attempt keeps 6 x 8 stage doubles
+// live across RHS evaluations that need ~100 registers of their own; at 2 waves per SIMD
+// (256 registers) the compiler spilled ~90 registers to scratch.  The reads take their
+// offset through an empty asm that depends on the stage just computed, so the compiler
+// neither forwards the stored registers (keeping them live) nor hoists the reads above
+// that RHS evaluation.  Values are stored and re-read unchanged: the arithmetic is the same.
+constexpr int KL_STRIDE = 256;
+__shared__ double kl_buf[4 * 8 * KL_STRIDE];  // 64 KB, allocated only in kernels that use it
+GDEV void kl_put(int j, const double* k, int D) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < D) kl_buf[(j * 8 + i) * KL_STRIDE + (int)threadIdx.x] = k[i];
+}
+// threadIdx.x, opaque to the compiler and ordered after `dep`
+GDEV int kl_slot_after(double dep) {
+  int t = (int)threadIdx.x;
+  __asm__ volatile("" : "+v"(t) : "v"(dep));
+  return t;
+}
+GDEV double kl_get(int t, int j, int i) { return kl_buf[(j * 8 + i) * KL_STRIDE + t]; }
+
 // QUAD: the Kerr-Schild RHS split over a quad (rhs_ks_quad), `sub` = lane & 3.
-template <int G, bool UNIT_H = false, bool QUAD = false>
+// KLDS: k1..k4 kept in LDS at kl (see kl_put).
+template <int G, bool UNIT_H = false, bool QUAD = false, bool KLDS = false>
 GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
                         double* yn, int sub = 0) {
   constexpr int D = Dim<G>::D;
   double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
+  int t = 0;  // LDS slot, re-derived after each stage (kl_slot_after)
+  // stage j's value k_j[i] (from LDS when parked there)
+#define KV(j, i) (KLDS ? kl_get(t, (j) - 1, (i)) : k##j[i])
   rhs_sel<G, QUAD>(S, rc, y, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k1[i] = UNIT_H ? o[i] : h * o[i];
+  if (KLDS) kl_put(0, k1, D);
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
   if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k2[i] = UNIT_H ? o[i] : h * o[i];
+  if (KLDS) {
+    kl_put(1, k2, D);
+    t = kl_slot_after(k2[D - 1]);
+  }
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * k1[i] + B32 * k2[i];
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * KV(1, i) + B32 * k2[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k3[i] = UNIT_H ? o[i] : h * o[i];
+  if (KLDS) {
+    kl_put(2, k3, D);
+    t = kl_slot_after(k3[D - 1]);
+  }
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * k1[i] + B42 * k2[i] + B43 * k3[i];
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * KV(1, i) + B42 * KV(2, i) + B43 * k3[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k4[i] = UNIT_H ? o[i] : h * o[i];
+  if (KLDS) {
+    kl_put(3, k4, D);
+    t = kl_slot_after(k4[D - 1]);
+  }
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * k1[i] + B52 * k2[i] + B53 * k3[i] + B54 * k4[i];
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * KV(1, i) + B52 * KV(2, i) + B53 * KV(3, i) + B54 * k4[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k5[i] = UNIT_H ? o[i] : h * o[i];
+  if (KLDS) t = kl_slot_after(k5[D - 1]);
 #pragma unroll
   for (int i = 0; i < D; ++i)
-    tmp[i] = y[i] + B61 * k1[i] + B62 * k2[i] + B63 * k3[i] + B64 * k4[i] + B65 * k5[i];
+    tmp[i] = y[i] + B61 * KV(1, i) + B62 * KV(2, i) + B63 * KV(3, i) + B64 * KV(4, i) + B65 * k5[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k6[i] = UNIT_H ? o[i] : h * o[i];
+  if (KLDS) t = kl_slot_after(k6[D - 1]);
   double e[8];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
-    yn[i] = y[i] + CH1 * k1[i] + CH2 * k2[i] + CH3 * k3[i] + CH4 * k4[i] + CH5 * k5[i] + CH6 * k6[i];
-    e[i] = CT1 * k1[i] + CT2 * k2[i] + CT3 * k3[i] + CT4 * k4[i] + CT5 * k5[i] + CT6 * k6[i];
+    const double a1 = KV(1, i), a2 = KV(2, i), a3 = KV(3, i), a4 = KV(4, i);
+    yn[i] = y[i] + CH1 * a1 + CH2 * a2 + CH3 * a3 + CH4 * a4 + CH5 * k5[i] + CH6 * k6[i];
+    e[i] = CT1 * a1 + CT2 * a2 + CT3 * a3 + CT4 * a4 + CT5 * k5[i] + CT6 * k6[i];
   }
+#undef KV
   if (D < 8) {
     yn[6] = 0.0;
     yn[7] = 0.0;
@@ -1212,6 +1258,8 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
   constexpr bool TAIL = (G == GRT_GEOM_KERR) && !VOL;
   const bool tail_on = TAIL && tl.cap != 0;
+  constexpr bool KLDS = ((GRT_KLDS_GEOMS) >> G) & 1;
+  if (tail_on && blockIdx.x == 0 && threadIdx.x == 0) tl.ctl[3] = __builtin_amdgcn_s_memrealtime();
 
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
@@ -1236,15 +1284,22 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
       uint64_t cnt = __popcll(need_mask);
       uint64_t remaining = chunk_end - chunk_next;
       uint64_t new_base = 0;
+      // Kerr-Schild claims exactly the items it starts now: a wave whose lanes are all busy
+      // with 1e6-step rays must not sit on unstarted items of a 64-item chunk (they would
+      // start only when one of its lanes frees up, possibly after the whole queue ran).
+      // Its rays are long, so the extra atomics are rare.
+      const uint64_t take = TAIL ? cnt - remaining : CHUNK;
       if (cnt > remaining) {
         unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(counter, (unsigned long long)CHUNK);
+        if (lane == 0) b = atomicAdd(counter, (unsigned long long)take);
         new_base = __shfl(b, 0);
       }
       if (need) {
         uint64_t rank = __popcll(need_mask & lanemask_lt);
         uint64_t item = rank < remaining ? chunk_next + rank : new_base + (rank - remaining);
         if (item >= n_items) {
+          if (TAIL && tail_on && !done && tl.ctl[4] == 0ull)
+            atomicCAS(&tl.ctl[4], 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
           done = true;
         } else {
           double row, col;
@@ -1295,7 +1350,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
       }
       if (cnt > remaining) {
         chunk_next = new_base + (cnt - remaining);
-        chunk_end = new_base + CHUNK;
+        chunk_end = new_base + take;
       } else {
         chunk_next += cnt;
       }
@@ -1314,7 +1369,10 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
           const uint64_t ev = __ballot(active);
           if (ev) {
             unsigned long long b = 0;
-            if (lane == 0) b = atomicAdd(&tl.ctl[1], (unsigned long long)__popcll(ev));
+            if (lane == 0) {
+              b = atomicAdd(&tl.ctl[1], (unsigned long long)__popcll(ev));
+              if (b == 0) tl.ctl[5] = __builtin_amdgcn_s_memrealtime();
+            }
             b = __shfl(b, 0);
             if (active) {
               const uint64_t e = b + __popcll(ev & lanemask_lt);
@@ -1350,7 +1408,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     constexpr bool UNIT_H_COPY = GRT_UNIT_H && G != GRT_GEOM_KERR;
     const double err_sq = (UNIT_H_COPY && __ballot(active && h_cur != 1.0) == 0)
                               ? rkf_attempt<G, UNIT_H_COPY>(S, rc, y, h_cur, yn)
-                              : rkf_attempt<G, false>(S, rc, y, h_cur, yn);
+                              : rkf_attempt<G, false, false, KLDS>(S, rc, y, h_cur, yn);
     n_att++;
     double h_next;
     const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
@@ -1475,6 +1533,7 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
     s.h_cur = rclamp(s.h, H_MIN, H_MAX);
   }
 
+  if (lane == 0) atomicMax(&tl.ctl[6], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   if (!writer) n_acc = n_att = 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {

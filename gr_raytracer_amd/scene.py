@@ -288,6 +288,19 @@ class Scene:
         L.check(L.lib().grt_tail_handoffs(self._s, device, C.byref(n)), "grt_tail_handoffs")
         return n.value
 
+    def tail_report(self, device: int = 0, capacity: int = 0) -> dict:
+        """Hand-off diagnostics of the last Kerr-Schild trace: count, timeline (s since the
+        integrate kernel started) and the handed-off rays' output slots and step counts."""
+        n = C.c_uint64()
+        tl = (C.c_double * 3)()
+        slot = np.zeros(capacity, np.uint64)
+        step = np.zeros(capacity, np.uint64)
+        L.check(L.lib().grt_tail_report(self._s, device, C.byref(n), tl, L.ptr(slot, C.c_uint64),
+                                        L.ptr(step, C.c_uint64), capacity), "grt_tail_report")
+        k = min(n.value, capacity)
+        return {"handed_off": n.value, "drained_s": tl[0], "handoff_s": tl[1], "tail_end_s": tl[2],
+                "slot": slot[:k], "step": step[:k]}
+
 
 def set_tail(threshold: int = -1) -> None:
     """Long-ray hand-off of Kerr-Schild traces (grt_set_tail): -1 auto, 0 off, > 0 the

@@ -532,6 +532,12 @@ int grt_set_tail(long long threshold);
 /* Rays the last Kerr-Schild trace on `device` handed to the tail kernel (synchronises the
  * device; 0 before the first trace).  A diagnostic of the scheduling above. */
 int grt_tail_handoffs(grt_scene* scene, int device, uint64_t* handed_off);
+/* The same plus the last trace's timeline in seconds since the integrate kernel started
+ * (queue drained, first hand-off, tail kernel end; 0 when not reached), and for the first
+ * min(handed_off, capacity) handed-off rays their output slot and the accepted steps
+ * they had taken (any pointer nullable). */
+int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double timeline_s[3], uint64_t* slot,
+                    uint64_t* step, uint64_t capacity);
 
 #ifdef __cplusplus
 }

@@ -24,11 +24,18 @@ n_shards = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 shards = [int(x) for x in sys.argv[2:]] or [0, n_shards // 2]
 for s in shards:
     t = time.time()
-    r = sc.render_shard(16, s, n_shards, aux=False)
+    r = sc.render_shard(16, s, n_shards, aux=True)
     st = r.stats
+    rep = sc.tail_report(capacity=1 << 20)
+    tail = {k: round(rep[k], 3) for k in ("drained_s", "handoff_s", "tail_end_s")}
+    if rep["handed_off"]:
+        rem = r.steps.astype("int64")[rep["slot"].astype("int64")] - rep["step"].astype("int64")
+        tail.update(max_remaining=int(rem.max()), mean_remaining=float(rem.mean()),
+                    longest_at_handoff=int(rep["step"][int(rem.argmax())]),
+                    us_per_step_tail=round((rep["tail_end_s"] - rep["handoff_s"]) * 1e6 / max(int(rem.max()), 1), 2))
     print(json.dumps({"shard": s, "n_shards": n_shards, "rays": st["rays"], "wall_s": round(time.time() - t, 3),
                       "kernel_ms": st["kernel_ms"], "accepted": st["accepted_steps"], "attempts": st["attempts"],
                       "steps_per_s": st["accepted_steps"] / (st["kernel_ms"] * 1e-3),
                       "overflows": st["hit_overflows"], "schedule": os.environ.get("GRT_SCHEDULE", "auto"),
-                      "tail": os.environ.get("GRT_TAIL", "auto"), "handoffs": sc.tail_handoffs(),
+                      "tail": os.environ.get("GRT_TAIL", "auto"), "handoffs": sc.tail_handoffs(), "tail_timeline": tail,
                       "md5": hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12]}), flush=True)

@@ -36,7 +36,9 @@ def load(pass_dir):
 def main():
     src, dst = Path(sys.argv[1]), Path(sys.argv[2])
     counters, kernel_ms = {}, {}
-    for p in ("fetch", "write", "valu", "busy"):
+    for p in ("fetch", "write", "valu", "busy", "mem"):
+        if not (src / p).exists():
+            continue
         vals, dur = load(src / p)
         for c, per in vals.items():
             counters[c] = sum(per.values()) / len(per)
