@@ -809,6 +809,51 @@ static int trace_common(grt_scene* s, int device, uint64_t n, bool camera, const
   return 0;
 }
 
+int grt_health_pixels(grt_scene* s, int device, uint32_t row0, uint32_t col0, uint32_t rows, uint32_t cols,
+                      grt_health* out, double* per_ray) {
+  if (!s || !out) return fail(-EINVAL, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  out->n_constants = s->desc.geometry == GRT_GEOM_KERR_BL ? 3u : 2u;
+  if ((uint64_t)row0 + rows > (uint64_t)s->desc.camera.rows || (uint64_t)col0 + cols > (uint64_t)s->desc.camera.cols)
+    return fail(-EINVAL, "rectangle outside the frame");
+  const uint64_t n = (uint64_t)rows * cols;
+  if (n == 0) return 0;
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  DevBuf b_out, b_status;
+  if ((rc = b_out.alloc(n * 5 * 8)) || (rc = b_status.alloc(n))) return rc;
+  grt::WorkList wl = rect_worklist(row0, col0, rows, cols);
+  HIP_TRY(grt::launch_health(s->desc.geometry, dc->d_scene, wl, n, (double*)b_out.p, (uint8_t*)b_status.p, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<double> v(n * 5);
+  std::vector<uint8_t> st(n);
+  HIP_TRY(hipMemcpy(v.data(), b_out.p, n * 5 * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(st.data(), b_status.p, n, hipMemcpyDeviceToHost));
+  // scene.rs:116-124 (error above 1e-10 for every ray) and report_drifts (integrator.rs:176-201,
+  // warnings above 1e-4 for the rays whose integration returned Ok)
+  for (uint64_t k = 0; k < n; ++k) {
+    const double* o = &v[k * 5];
+    out->rays++;
+    if (!(o[0] < 1e-10)) out->null_violations++;
+    out->max_null = std::fmax(out->max_null, o[0]);
+    if (st[k] != GRT_OK) {
+      out->failed++;
+      continue;
+    }
+    if (o[1] > 1e-4) out->kk_drift_rays++;
+    out->max_kk_drift = std::fmax(out->max_kk_drift, o[1]);
+    for (uint32_t c = 0; c < out->n_constants; ++c) {
+      if (o[2 + c] > 1e-4) out->constant_drift_rays[c]++;
+      out->max_constant_drift[c] = std::fmax(out->max_constant_drift[c], o[2 + c]);
+    }
+  }
+  if (per_ray) std::memcpy(per_ray, v.data(), n * 5 * 8);
+  return 0;
+}
+
 int grt_trace_pixels(grt_scene* s, int device, uint64_t n, const double* rows, const double* cols,
                      uint64_t capacity, double* steps_out, uint64_t* n_steps, uint8_t* stop_out,
                      uint8_t* status_out) {

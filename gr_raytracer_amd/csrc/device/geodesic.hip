@@ -1633,6 +1633,157 @@ hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const Traj
   return hipGetLastError();
 }
 
+// ====================================================== invariant monitors =======
+// The reference's per-ray health checks, off the render path:
+//  * the null condition of the camera ray, |k.k| < 1e-10 (scene.rs:116-124, logged as an
+//    error otherwise);
+//  * in debug builds, the largest |k.k| over the accepted steps and the largest drift of
+//    each constant of motion from its value at step 0, relative when |initial| > 1e-12
+//    (integrator.rs:91-146), warned above 1e-4 (report_drifts, :176-201).  A ray whose
+//    rkf45 fails returns Err before report_drifts: it reports no drift.
+// health_kernel re-integrates the rays (one lane per ray) with these monitors.
+
+// get_constants_of_motion at (x, p): E, L_z and, for KerrBL, Carter's Q.  Returns the count.
+template <int G>
+GDEV int constants_of_motion(const DevScene& S, const double* x, const double* p, double* c) {
+  if constexpr (G == GRT_GEOM_EUCLIDEAN) {  // euclidean.rs:160-182
+    const double p_x = -p[1], p_y = -p[2];
+    c[0] = p[0];
+    c[1] = x[1] * p_y - x[2] * p_x;
+    return 2;
+  } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:147-166
+    const double r = x[1], st = rsin(x[2]);
+    c[0] = p[0];
+    c[1] = -r * r * st * st * p[3];
+    return 2;
+  } else if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {  // schwarzschild.rs:213-233
+    const double r = x[1], st = rsin(x[2]);
+    const double a = 1.0 - S.radius / r;
+    c[0] = a * p[0];
+    c[1] = -r * r * st * st * p[3];
+    return 2;
+  } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:421-445
+    double g[4][4], pc[4];
+    ks_metric(S.radius, S.a, x[1], x[2], x[3], g);
+    mat_vec(g, p, pc);
+    c[0] = -pc[0];
+    c[1] = -x[2] * pc[1] + x[1] * pc[2];
+    return 2;
+  } else {  // KerrBL, kerr_bl.rs:596-625 (metric_bl's and this sin / cos of one theta: one sincos)
+    double st, ct;
+    rsincos(x[2], &st, &ct);
+    double g[4][4], pc[4];
+    metric_bl(S.radius, S.a, x[1], st, ct, g);
+    mat_vec(g, p, pc);
+    const double e = -pc[0], l_z = pc[3], p_theta = pc[2];
+    const double sin2 = st * st;
+    c[0] = e;
+    c[1] = l_z;
+    c[2] = p_theta * p_theta + ct * ct * (l_z * l_z / fmax(sin2, 1e-28) - S.a * S.a * e * e);
+    return 3;
+  }
+}
+// inner_product(x, v, v) at a native-chart point
+template <int G>
+GDEV double inner_at(const DevScene& S, const double* x, const double* v) {
+  double st = 0.0, ct = 0.0;
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) st = rsin(x[2]);
+  else if constexpr (G == GRT_GEOM_KERR_BL) rsincos(x[2], &st, &ct);
+  return inner<G>(S, x, st, ct, v, v);
+}
+GDEV double drift_of(double cur, double init) {  // integrator.rs:127-134
+  return fabs(init) > 1e-12 ? fabs(cur - init) / fabs(init) : fabs(cur - init);
+}
+
+// Per ray k (pixel (row0 + k / cols, col0 + k % cols)): out[k * 5 + 0] |k.k| of the camera
+// ray, [1] the largest |k.k| over the accepted steps, [2..4] the largest drift of E, L_z, Q;
+// status[k] = GRT_ERR_MAX_STEPS_REACHED when rkf45 failed (no drift report).
+template <int G>
+__global__ void __launch_bounds__(64) health_kernel(const DevScene* __restrict__ Sp, WorkList wl, uint64_t n,
+                                                    double* __restrict__ out, uint8_t* __restrict__ status) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before the early return
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double row = (double)(wl.row0 + (uint32_t)(k / wl.cols)), col = (double)(wl.col0 + (uint32_t)(k % wl.cols));
+  double pcam[4];
+  camera_momentum(S.cam, row, col, pcam);
+  const double null_kk = fabs(inner<G>(S, S.cam.pos, S.cam.sin_theta, S.cam.cos_theta, pcam, pcam));
+  double y[8];
+  RayConst rc;
+  init_ray<G>(S, row, col, y, rc);
+  double p[4], c0[3] = {0.0, 0.0, 0.0}, c1[3];
+  momentum<G>(S, rc, y, p);
+  const int nc = constants_of_motion<G>(S, y, p, c0);
+  double max_kk = 0.0, max_d[3] = {0.0, 0.0, 0.0};
+  int st_out = GRT_OK;
+  double h = S.step_size;
+  for (uint64_t i = 1; i < S.max_steps; ++i) {
+    double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
+    int retries = 0, ctl;
+    do {
+      const double err_sq = rkf_attempt<G>(S, rc, y, h_cur, yn);
+      ctl = step_control(S, err_sq, h_cur, retries, h_next);
+    } while (ctl == STEP_RETRY);
+    if (ctl == STEP_FAILED) {
+      st_out = GRT_ERR_MAX_STEPS_REACHED;
+      break;
+    }
+    h = h_next;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) y[q] = yn[q];
+    momentum<G>(S, rc, y, p);
+    const double kk = fabs(inner_at<G>(S, y, p));
+    if (kk > max_kk) max_kk = kk;
+    constants_of_motion<G>(S, y, p, c1);
+    for (int q = 0; q < nc; ++q) {
+      const double d = drift_of(c1[q], c0[q]);
+      if (d > max_d[q]) max_d[q] = d;
+    }
+    double c[3];
+    bool c_valid = false;
+    if (should_stop<G>(S, y, c, c_valid, i) != GRT_STOP_NONE) break;
+  }
+  double* o = out + k * 5;
+  o[0] = null_kk;
+  o[1] = max_kk;
+  o[2] = max_d[0];
+  o[3] = max_d[1];
+  o[4] = max_d[2];
+  status[k] = (uint8_t)st_out;
+}
+
+hipError_t launch_health(int geometry, const DevScene* d_scene, const WorkList& wl, uint64_t n, double* d_out,
+                         uint8_t* d_status, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((n + 63) / 64);
+  switch (geometry) {
+    case GRT_GEOM_EUCLIDEAN:
+      hipLaunchKernelGGL(health_kernel<GRT_GEOM_EUCLIDEAN>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n, d_out,
+                         d_status);
+      break;
+    case GRT_GEOM_SCHWARZSCHILD:
+      hipLaunchKernelGGL(health_kernel<GRT_GEOM_SCHWARZSCHILD>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n,
+                         d_out, d_status);
+      break;
+    case GRT_GEOM_KERR:
+      hipLaunchKernelGGL(health_kernel<GRT_GEOM_KERR>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n, d_out,
+                         d_status);
+      break;
+    case GRT_GEOM_KERR_BL:
+      hipLaunchKernelGGL(health_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, wl, n, d_out,
+                         d_status);
+      break;
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL:
+      hipLaunchKernelGGL(health_kernel<GRT_GEOM_EUCLIDEAN_SPHERICAL>, dim3(blocks), dim3(64), 0, stream, d_scene, wl,
+                         n, d_out, d_status);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 // ============================================================ probe kernel =======
 // Work-order probe (scheduling only, never an output): one ray per 8x8 tile, the
 // tile's pixel (3, 3), integrated for at most `cap` accepted steps.  A frame's cost is

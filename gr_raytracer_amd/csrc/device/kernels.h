@@ -44,6 +44,11 @@ struct TrajectoryList {
 };
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
 
+// Invariant monitors of the n = rows x cols rays of a rectangle (health_kernel):
+// d_out n x 5 doubles, d_status n bytes.
+hipError_t launch_health(int geometry, const DevScene* d_scene, const WorkList& wl, uint64_t n, double* d_out,
+                         uint8_t* d_status, hipStream_t stream);
+
 // Adaptive supersampling helpers (raytracer.rs:91-159, :320-458).
 struct AdaptiveParams {
   uint32_t w, h;  // section size

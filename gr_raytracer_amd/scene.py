@@ -282,6 +282,27 @@ class Scene:
         r = self.render_pixels(row, col, 1, 1, device=device)
         return r.xyza64[0], int(r.ray_class[0]), int(r.status[0])
 
+    def health(self, row0: int = 0, col0: int = 0, rows: Optional[int] = None, cols: Optional[int] = None,
+               device: int = 0, per_ray: bool = False) -> dict:
+        """The reference's invariant monitors over a rectangle (grt_health_pixels): camera-ray
+        null condition (scene.rs:116-124) and k.k / constants-of-motion drifts
+        (integrator.rs:91-201).  per_ray adds an (n, 5) array: |k.k| at the camera, largest
+        |k.k| along the path, largest drift of E, L_z, Q."""
+        rows = self.rows - row0 if rows is None else rows
+        cols = self.cols - col0 if cols is None else cols
+        h = L.Health()
+        arr = np.zeros((rows * cols, 5)) if per_ray else None
+        L.check(L.lib().grt_health_pixels(self._s, device, row0, col0, rows, cols, C.byref(h),
+                                          L.ptr(arr, C.c_double) if per_ray else None), "grt_health_pixels")
+        nc = h.n_constants
+        out = {"rays": h.rays, "failed": h.failed, "null_violations": h.null_violations, "max_null": h.max_null,
+               "kk_drift_rays": h.kk_drift_rays, "max_kk_drift": h.max_kk_drift, "n_constants": nc,
+               "constant_drift_rays": list(h.constant_drift_rays)[:nc],
+               "max_constant_drift": list(h.max_constant_drift)[:nc]}
+        if per_ray:
+            out["per_ray"] = arr
+        return out
+
     def tail_handoffs(self, device: int = 0) -> int:
         """Rays the last Kerr-Schild trace on `device` handed to the tail kernel."""
         n = C.c_uint64()

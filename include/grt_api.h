@@ -484,6 +484,33 @@ int grt_trace_rays(grt_scene* scene, int device, uint64_t n, const double* posit
                    const double* momenta, uint64_t capacity, double* steps_out,
                    uint64_t* n_steps, uint8_t* stop_out, uint8_t* status_out);
 
+/* ---- invariant monitors (off the render path) --------------------------------- */
+/* The reference's per-ray health checks over a rows x cols rectangle, re-integrating
+ * each ray with the monitors on:
+ *  - the null condition of the camera ray: Scene::color_of_ray logs an error when
+ *    |k.k| >= 1e-10 (scene.rs:116-124);
+ *  - the debug-build drift monitors of Integrator::integrate (integrator.rs:91-146): the
+ *    largest |k.k| over the accepted steps and the largest drift of each constant of
+ *    motion (get_constants_of_motion: E, L_z, and Carter's Q for KerrBL) from its value at
+ *    step 0, relative when |initial| > 1e-12, warned above 1e-4 (report_drifts, :176-201).
+ *    Rays whose rkf45 fails return Err before report_drifts and report no drift. */
+typedef struct grt_health {
+  uint64_t rays;
+  uint64_t failed;                 /* rkf45 Err (MaxStepsReached): no drift report          */
+  uint64_t null_violations;        /* camera rays with |k.k| >= 1e-10                        */
+  double max_null;                 /* largest |k.k| of a camera ray                         */
+  uint64_t kk_drift_rays;          /* rays whose largest |k.k| along the path > 1e-4         */
+  double max_kk_drift;
+  uint32_t n_constants;            /* 2 (E, L_z) or 3 (KerrBL: E, L_z, Q)                    */
+  uint32_t _pad;
+  uint64_t constant_drift_rays[3]; /* rays whose drift of constant c > 1e-4                  */
+  double max_constant_drift[3];
+} grt_health;
+/* per_ray (nullable): rows*cols x 5 doubles -- |k.k| of the camera ray, largest |k.k| along
+ * the path, largest drift of E, L_z, Q (0 where not defined). */
+int grt_health_pixels(grt_scene* scene, int device, uint32_t row0, uint32_t col0, uint32_t rows,
+                      uint32_t cols, grt_health* out, double* per_ray);
+
 /* render_ray_at's initial ray (cli/{euclidean,schwarzschild,kerr,kerr_bl}.rs): the unit
  * spatial `direction` in the local tetrad at the Cartesian `position` (t = 0), as a
  * native-chart position and contravariant momentum for grt_trace_rays.  -EINVAL when

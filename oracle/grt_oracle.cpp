@@ -325,6 +325,8 @@ struct Geometry {  // geometry.rs:108-121 + SupportQuantities :49-81
   virtual double radial_coordinate(const Point& p) const = 0;
   virtual FourVector stationary_velocity(const Point& p) const = 0;
   virtual Err circular_orbit_velocity(const Point& p, FourVector* out) const = 0;
+  // get_constants_of_motion (geometry.rs:119-120): E, L_z (+ Q); returns the count
+  virtual int constants_of_motion(const Point& p, const FourVector& m, double* c) const = 0;
   Point make_point(const double* y) const { return Point{cs(), a, {y[0], y[1], y[2], y[3]}}; }
 };
 
@@ -356,6 +358,12 @@ struct Euclidean : Geometry {
   Err circular_orbit_velocity(const Point&, FourVector* out) const override {
     *out = FourVector{CS::Cartesian, {1.0, 0.0, 0.0, 0.0}};
     return OK;
+  }
+  int constants_of_motion(const Point& p, const FourVector& m, double* c) const override {  // :160-182
+    double p_x = -m[1], p_y = -m[2];
+    c[0] = m[0];
+    c[1] = p[1] * p_y - p[2] * p_x;
+    return 2;
   }
 };
 
@@ -417,6 +425,13 @@ struct Schwarzschild : Geometry {
     *out = FourVector{CS::Spherical, {c.u_t, 0.0, 0.0, c.u_phi}};
     return OK;
   }
+  int constants_of_motion(const Point& p, const FourVector& m, double* c) const override {  // :213-233
+    double r = p[1], theta = p[2];  // a lone sin in this function
+    double a = 1.0 - radius / r;
+    c[0] = a * m[0];
+    c[1] = -r * r * g_sin(theta) * g_sin(theta) * m[3];
+    return 2;
+  }
 };
 
 // ---- EuclideanSpherical: flat space in the spherical chart (geometry/euclidean_spherical.rs) ----
@@ -460,6 +475,12 @@ struct EuclideanSpherical : Geometry {
   Err circular_orbit_velocity(const Point&, FourVector* out) const override {  // :177-183
     *out = FourVector{CS::Spherical, {1.0, 0.0, 0.0, 0.0}};
     return OK;
+  }
+  int constants_of_motion(const Point& p, const FourVector& m, double* c) const override {  // :147-166
+    double r = p[1], theta = p[2];
+    c[0] = m[0];
+    c[1] = -r * r * g_sin(theta) * g_sin(theta) * m[3];
+    return 2;
   }
 };
 
@@ -615,6 +636,14 @@ struct Kerr : Geometry {
     *out = u;
     return OK;
   }
+  int constants_of_motion(const Point& p, const FourVector& m, double* c) const override {  // :421-445
+    Mat4 g = ks_metric(radius, a, p[1], p[2], p[3]);
+    double pc[4];
+    mat_vec(g, m.v, pc);  // nalgebra Matrix4 * Vector4
+    c[0] = -pc[0];
+    c[1] = -p[2] * pc[1] + p[1] * pc[2];
+    return 2;
+  }
 };
 
 // ---- KerrBL, Boyer-Lindquist with Carter constant (geometry/kerr_bl.rs) ----
@@ -747,6 +776,20 @@ struct KerrBL : Geometry {
     if (e != OK) return e;
     *out = FourVector{CS::BoyerLindquist, {c.u_t, 0.0, 0.0, c.u_phi}};
     return OK;
+  }
+  int constants_of_motion(const Point& p, const FourVector& m, double* c) const override {  // :596-625
+    double r = p[1], theta = p[2];
+    Mat4 g = metric_bl(radius, a, r, theta);
+    double pc[4];
+    mat_vec(g, m.v, pc);
+    double e = -pc[0], l_z = pc[3], p_theta_cov = pc[2];
+    double sin_t, cos_t;  // theta.cos() and theta.sin() in one function: one sincos
+    g_sincos(theta, &sin_t, &cos_t);
+    double sin2 = sin_t * sin_t;  // powi(2)
+    c[0] = e;
+    c[1] = l_z;
+    c[2] = p_theta_cov * p_theta_cov + cos_t * cos_t * (l_z * l_z / std::fmax(sin2, 1e-28) - a * a * e * e);
+    return 3;
   }
 };
 
@@ -1809,6 +1852,43 @@ int oracle_color_of_ray(const grt_scene_desc* d, int64_t row, int64_t col, int u
   if (steps) *steps = cnt.accepted;
   if (attempts) *attempts = cnt.attempts;
   return 0;
+}
+
+// The reference's invariant monitors per camera ray of a rectangle (scene.rs:116-124,
+// integrator.rs:91-146): out[k * 5] |k.k| of the camera ray, [1] the largest |k.k| over the
+// accepted steps, [2..4] the largest drift of each constant of motion from step 0
+// (relative when |initial| > 1e-12); status[k] = the integration error (no drift report).
+void oracle_health_pixels(const grt_scene_desc* d, uint32_t row0, uint32_t col0, uint32_t rows, uint32_t cols,
+                          int threads, double* out, uint8_t* status) {
+  SceneCtx S;
+  init_ctx(S, d);
+  const uint64_t n = (uint64_t)rows * cols;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1)
+  for (int64_t k = 0; k < (int64_t)n; ++k) {
+    const Geometry& g = *S.g;
+    Ray ray = make_ray(S, row0 + k / cols, col0 + k % cols, false, 0.0, 0.0);
+    double* o = out + k * 5;
+    for (int q = 0; q < 5; ++q) o[q] = 0.0;
+    o[0] = std::fabs(g.inner_product(ray.position, ray.momentum, ray.momentum));
+    std::vector<Step> steps;
+    int stop;
+    Counters cnt;
+    Err e = integrate(g, S.cfg, ray, steps, &stop, &cnt);
+    status[k] = (uint8_t)e;
+    if (e != OK) continue;
+    double c0[3] = {0, 0, 0}, c1[3];
+    const int nc = g.constants_of_motion(steps[0].x, steps[0].p, c0);
+    for (size_t i = 1; i < steps.size(); ++i) {
+      double kk = std::fabs(g.inner_product(steps[i].x, steps[i].p, steps[i].p));
+      if (kk > o[1]) o[1] = kk;
+      g.constants_of_motion(steps[i].x, steps[i].p, c1);
+      for (int q = 0; q < nc; ++q) {
+        double drift = std::fabs(c0[q]) > 1e-12 ? std::fabs(c1[q] - c0[q]) / std::fabs(c0[q])
+                                                 : std::fabs(c1[q] - c0[q]);
+        if (drift > o[2 + q]) o[2 + q] = drift;
+      }
+    }
+  }
 }
 
 // render_section_to_cie_buffer_raw (raytracer.rs:195-244) over a rectangle, or over an

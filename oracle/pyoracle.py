@@ -37,6 +37,7 @@ def lib():
         L.oracle_render_pixels.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, _u32p,
                                            _pd, _pd, _u32p, C.c_uint32, _pd, _u8p, _u8p, _u8p, _u32p, C.c_int,
                                            _u64p, _u64p]
+        L.oracle_health_pixels.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, _pd, _u8p]
         L.oracle_render_section.restype = C.c_uint64
         L.oracle_render_section.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, _pd, _pd, _u8p,
                                             C.c_int]
@@ -128,6 +129,16 @@ def render_pixels(desc, row0, col0, rows, cols, threads=8, offsets=None, row_lis
                                       threads, C.byref(acc), C.byref(att))
     return {"xyza": xyza, "ray_class": cls, "status": st, "stop": stop, "steps": steps, "wall_s": wall,
             "accepted": acc.value, "attempts": att.value}
+
+
+def health_pixels(desc, row0, col0, rows, cols, threads=8):
+    """Per-ray invariant monitors (scene.rs:116-124, integrator.rs:91-146): (n, 5) array of
+    |k.k| at the camera, largest |k.k| along the path, largest drift of E, L_z, Q; status."""
+    n = rows * cols
+    out = np.zeros((n, 5))
+    st = np.zeros(n, np.uint8)
+    lib().oracle_health_pixels(_addr(desc), row0, col0, rows, cols, threads, _dp(out), st.ctypes.data_as(_u8p))
+    return out, st
 
 
 def render_section(desc, from_row, from_col, to_row, to_col, adaptive, mask=None, threads=8):
