@@ -49,7 +49,9 @@ FP64_MEASURED_PEAK_TFLOPS = 61.8  # tools/fp64_peak.hip, profiles/r01/fp64_peak.
 FP64_NO_CONTRACTION_TFLOPS = FP64_VECTOR_PEAK_TFLOPS / 2
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table
 BYTES_PER_PIXEL_OUT = 16 + 1 + 1  # f32 XYZA + class + status
-PMC_FILE = {"c2": ROOT / "profiles" / "r02_c2_pmc.json", "c4": ROOT / "profiles" / "r02_c4_pmc.json"}
+# the kernel whose PMC summary (profiles/*_pmc.json, tools/pmc_summary.py) gives `traffic`
+PMC_DIR = ROOT / "profiles"
+PMC_KERNEL = {"c2": "grt::integrate_kernel<1, false>", "c4": "grt::integrate_kernel<2, false>"}
 SCENES = ROOT / "tests" / "golden" / "scenes"
 
 
@@ -156,6 +158,31 @@ def cpu_baseline(g, workload: str = "c2") -> dict:
 
 
 # ------------------------------------------------------------------- roofline ----
+def find_pmc(workload: str):
+    """The newest PMC summary under profiles/ that measured THIS build's code of the
+    workload's integrate kernel (kernel_code_sha256, or the whole device code's hash for
+    summaries that predate it).  Returns (path, summary, note)."""
+    from gr_raytracer_amd import _lib as L
+
+    kname = PMC_KERNEL[workload]
+    mine_k = L.kernel_code_sha256(L.kernel_symbol(kname))
+    mine_all = L.device_code_sha256()
+    stale = []
+    for prof in sorted(PMC_DIR.glob("*_pmc.json"), reverse=True):
+        try:
+            pmc = json.loads(prof.read_text())
+        except ValueError:
+            continue
+        if not pmc.get("kernel", "").startswith(kname + ","):
+            continue
+        if pmc.get("kernel_code_sha256") == mine_k or pmc.get("code_object_sha256") == mine_all:
+            return prof, pmc, None
+        stale.append(prof.name)
+    if stale:
+        return None, None, f"PMC summaries of {kname} ({', '.join(stale[:3])}) measured another build: not used"
+    return None, None, f"no PMC summary of {kname}"
+
+
 def roofline(workload: str, geometry: str, accepted: float, attempts: float, kernel_ms: float,
              n_pixels: int, kernel_name: str) -> dict:
     """FP64 VALU roofline of the integrate kernel for one launch (counts per launch)."""
@@ -172,21 +199,16 @@ def roofline(workload: str, geometry: str, accepted: float, attempts: float, ker
            "flop_model": f"{f_att:g}*attempts + {f_step:g}*accepted (SURVEY 8d)",
            "hbm_algorithmic_GBps": n_pixels * BYTES_PER_PIXEL_OUT / (kernel_ms * 1e-3) / 1e9,
            "hbm_peak_GBps": HBM_PEAK_GBS}
-    prof = PMC_FILE.get(workload)
-    if prof is not None and prof.exists():
-        pmc = json.loads(prof.read_text())
-        mine = L.device_code_sha256()
-        if pmc.get("code_object_sha256") != mine:
-            out["traffic_note"] = f"{prof.name} was taken from another build of the device code: not used"
-        else:
-            out["traffic"] = pmc.get("hbm_bytes_per_launch")
-            out["pmc_file"] = os.path.relpath(prof, ROOT)
-            for k in ("active_valu_over_wave_cycles", "lane_utilisation", "valu_f64_fraction",
-                      "wait_inst_any_over_wave_cycles", "scratch_bytes_per_launch"):
-                if k in pmc:
-                    out[k] = pmc[k]
+    prof, pmc, note = find_pmc(workload)
+    if pmc is None:
+        out["traffic_note"] = note
     else:
-        out["traffic_note"] = "no PMC summary for this workload"
+        out["traffic"] = pmc.get("hbm_bytes_per_launch")
+        out["pmc_file"] = os.path.relpath(prof, ROOT)
+        for k in ("active_valu_over_wave_cycles", "lane_utilisation", "valu_f64_fraction",
+                  "wait_inst_any_over_wave_cycles", "scratch_bytes_per_launch"):
+            if k in pmc:
+                out[k] = pmc[k]
     return out
 
 

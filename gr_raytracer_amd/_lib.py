@@ -291,3 +291,129 @@ def device_code_sha256(path: Path = LIB_PATH) -> str:
         if data[str_off + name:end] == b".hip_fatbin":
             return hashlib.sha256(data[off:off + size]).hexdigest()
     raise GrtError(f"{path}: no .hip_fatbin section")
+
+
+def _elf_sections(data: bytes, base: int = 0):
+    """{name: (offset, size, link, entsize)} of an ELF64 image starting at data[base:]."""
+    import struct
+
+    shoff, = struct.unpack_from("<Q", data, base + 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, base + 0x3A)
+    raw = [struct.unpack_from("<IIQQQQIIQQ", data, base + shoff + i * shentsize) for i in range(shnum)]
+    str_off = base + raw[shstrndx][4]
+    out = {}
+    for name, _t, _f, _a, off, size, link, _info, _al, entsize in raw:
+        nm = data[str_off + name:data.index(b"\0", str_off + name)].decode()
+        out[nm] = (base + off, size, raw[link][4] + base if link < len(raw) else 0, entsize)
+    return out
+
+
+def _mask_pc_relative(code: bytearray) -> None:
+    """Zero the link-time displacements of `s_getpc_b64; s_add_u32 lit; s_addc_u32 lit`
+    (the address of a global table: they move when other kernels change size)."""
+    import struct
+
+    for i in range(0, len(code) - 20, 4):
+        w0, w1, _, w3 = struct.unpack_from("<IIII", code, i)
+        if (w0 & 0xFF80FF00) == 0xBE801C00 and (w1 >> 24) == 0x80 and ((w1 >> 8) & 0xFF) == 0xFF \
+                and (w3 >> 24) == 0x82 and ((w3 >> 8) & 0xFF) == 0xFF:
+            code[i + 8:i + 12] = bytes(4)
+            code[i + 16:i + 20] = bytes(4)
+
+
+def kernel_code_sha256(symbol: str, path: Path = LIB_PATH) -> str:
+    """SHA-256 of ONE kernel's gfx950 machine code and kernel descriptor inside
+    libgrt.so: the bytes of the function symbol `symbol` (mangled name) and of
+    `symbol.kd` in the gfx950 code object of the `.hip_fatbin` offload bundle.  A PMC
+    summary records it for the kernel it measured, so adding or changing an unrelated
+    kernel does not invalidate it (a change of this kernel's code, register counts or
+    LDS size does)."""
+    import hashlib
+    import struct
+
+    data = Path(path).read_bytes()
+    fb_off, fb_size, _, _ = _elf_sections(data)[".hip_fatbin"]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    if data[fb_off:fb_off + len(magic)] != magic:
+        raise GrtError(f"{path}: .hip_fatbin is not an uncompressed offload bundle")
+    p = fb_off + len(magic)
+    n, = struct.unpack_from("<Q", data, p)
+    p += 8
+    co = None
+    for _ in range(n):
+        off, size, tlen = struct.unpack_from("<QQQ", data, p)
+        triple = data[p + 24:p + 24 + tlen].decode()
+        p += 24 + tlen
+        if "gfx950" in triple:
+            co = fb_off + off
+    if co is None:
+        raise GrtError(f"{path}: no gfx950 code object in the bundle")
+    secs = _elf_sections(data, co)
+    sym_off, sym_size, str_off, entsize = secs[".symtab"]
+    h = hashlib.sha256()
+    found = 0
+    for want in (symbol, symbol + ".kd"):
+        for k in range(sym_size // entsize):
+            st_name, st_info, _o, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", data, sym_off + k * entsize)
+            nm = data[str_off + st_name:data.index(b"\0", str_off + st_name)].decode()
+            if nm != want:
+                continue
+            # locate the symbol's bytes through its section's address/offset
+            shoff, = struct.unpack_from("<Q", data, co + 0x28)
+            shentsize, = struct.unpack_from("<H", data, co + 0x3A)
+            _n, _t, _f, s_addr, s_off, _s, _l, _i, _al, _e = struct.unpack_from("<IIQQQQIIQQ", data,
+                                                                                  co + shoff + st_shndx * shentsize)
+            start = co + s_off + (st_value - s_addr)
+            body = bytearray(data[start:start + st_size])
+            if want.endswith(".kd"):
+                body[16:24] = bytes(8)  # kernel_code_entry_byte_offset: where the linker placed the code
+            else:
+                _mask_pc_relative(body)
+            h.update(want.encode() + b"\0" + bytes(body))
+            found += 1
+            break
+    if found != 2:
+        raise GrtError(f"{path}: kernel symbol {symbol} (and its .kd) not found")
+    return h.hexdigest()
+
+
+def kernel_symbols(path: Path = LIB_PATH) -> list:
+    """Mangled names of the kernels in libgrt.so's gfx950 code object."""
+    import struct
+
+    data = Path(path).read_bytes()
+    fb_off, _, _, _ = _elf_sections(data)[".hip_fatbin"]
+    p = fb_off + 24
+    n, = struct.unpack_from("<Q", data, p)
+    p += 8
+    co = None
+    for _ in range(n):
+        off, size, tlen = struct.unpack_from("<QQQ", data, p)
+        if "gfx950" in data[p + 24:p + 24 + tlen].decode():
+            co = fb_off + off
+        p += 24 + tlen
+    sym_off, sym_size, str_off, entsize = _elf_sections(data, co)[".symtab"]
+    out = []
+    for k in range(sym_size // entsize):
+        st_name, = struct.unpack_from("<I", data, sym_off + k * entsize)
+        nm = data[str_off + st_name:data.index(b"\0", str_off + st_name)].decode()
+        if nm.endswith(".kd"):
+            out.append(nm[:-3])
+    return out
+
+
+def kernel_symbol(demangled: str, path: Path = LIB_PATH) -> str:
+    """Mangled name of a `grt::name<int-or-bool, ...>` kernel, e.g.
+    "grt::integrate_kernel<1, false>" -> "_ZN3grt16integrate_kernelILi1ELb0EE..."."""
+    import re
+
+    m = re.fullmatch(r"grt::(\w+)<([^>]*)>", demangled.strip())
+    if not m:
+        raise GrtError(f"cannot mangle {demangled!r}")
+    name, args = m.group(1), [a.strip() for a in m.group(2).split(",")]
+    enc = "".join("Lb1E" if a == "true" else "Lb0E" if a == "false" else f"Li{int(a)}E" for a in args)
+    prefix = f"_ZN3grt{len(name)}{name}I{enc}E"
+    hits = [k for k in kernel_symbols(path) if k.startswith(prefix)]
+    if len(hits) != 1:
+        raise GrtError(f"{demangled}: {len(hits)} matching kernel symbols")
+    return hits[0]

@@ -113,14 +113,23 @@ def test_host_cores_census():
 def test_roofline_refuses_pmc_of_another_build(grt, tmp_path, monkeypatch):
     import bench
 
-    pmc = tmp_path / "pmc.json"
-    pmc.write_text(json.dumps({"code_object_sha256": "0" * 64, "hbm_bytes_per_launch": 1.0}))
-    monkeypatch.setitem(bench.PMC_FILE, "c2", pmc)
+    kname = bench.PMC_KERNEL["c2"]
+    pmc = tmp_path / "r99_c2_pmc.json"
+    pmc.write_text(json.dumps({"kernel": kname + ", test", "code_object_sha256": "0" * 64,
+                               "kernel_code_sha256": "1" * 64, "hbm_bytes_per_launch": 1.0}))
+    monkeypatch.setattr(bench, "PMC_DIR", tmp_path)
     r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")
     assert r["traffic"] is None and "another build" in r["traffic_note"]
     assert abs(r["frac"] * bench.FP64_VECTOR_PEAK_TFLOPS - r["achieved"]) < 1e-9
     assert abs(r["frac_no_contraction"] - 2 * r["frac"]) < 1e-12
-    pmc.write_text(json.dumps({"code_object_sha256": grt._lib.device_code_sha256(), "hbm_bytes_per_launch": 7.0,
-                               "lane_utilisation": 0.9}))
+    # a summary of another kernel is never used, whatever its hashes
+    (tmp_path / "r99_c4_pmc.json").write_text(json.dumps({
+        "kernel": bench.PMC_KERNEL["c4"] + ", test", "code_object_sha256": grt._lib.device_code_sha256(),
+        "hbm_bytes_per_launch": 3.0}))
+    assert bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")["traffic"] is None
+    # the per-kernel hash of this build's kernel is accepted
+    pmc.write_text(json.dumps({"kernel": kname + ", test", "code_object_sha256": "0" * 64,
+                               "kernel_code_sha256": grt._lib.kernel_code_sha256(grt._lib.kernel_symbol(kname)),
+                               "hbm_bytes_per_launch": 7.0, "lane_utilisation": 0.9}))
     r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")
     assert r["traffic"] == 7.0 and r["lane_utilisation"] == 0.9

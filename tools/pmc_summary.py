@@ -13,7 +13,7 @@ from collections import defaultdict
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from gr_raytracer_amd._lib import device_code_sha256  # noqa: E402
+from gr_raytracer_amd._lib import device_code_sha256, kernel_code_sha256, kernel_symbol  # noqa: E402
 
 KERNEL = sys.argv[3] if len(sys.argv) > 3 else "grt::integrate_kernel<1, false>"
 WORKLOAD = sys.argv[4] if len(sys.argv) > 4 else "one frame of tools/prof_target.py c2 (1500x1500, 2.25M rays)"
@@ -50,6 +50,9 @@ def main():
         "kernel": f"{KERNEL}, {WORKLOAD}",
         # the device code the passes measured: bench.py refuses a summary of another build
         "code_object_sha256": device_code_sha256(),
+        # this kernel's own code + descriptor (PC-relative displacements masked): stays
+        # valid while other kernels change
+        "kernel_code_sha256": kernel_code_sha256(kernel_symbol(KERNEL)),
         "source": "rocprofv3 --kernel-trace --pmc <one counter group per pass>, tools/run_pmc.sh",
         "counters": counters,
         "kernel_ms_per_pass": kernel_ms,
