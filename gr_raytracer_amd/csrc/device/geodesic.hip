@@ -46,6 +46,9 @@ namespace grt {
 #ifndef GRT_KLDS_GEOMS
 #define GRT_KLDS_GEOMS (1 << GRT_GEOM_KERR)  // integrate kernels whose RKF stages k1..k4 live in LDS
 #endif
+#ifndef GRT_KL_STAGES
+#define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
+#endif
 
 // f64::powf == glibc pow: bit-exact on glibc's fast path, OCML outside it.
 GDEV double rpow(double x, double y) {
@@ -450,7 +453,7 @@ struct Dim {
 // neither forwards the stored registers (keeping them live) nor hoists the reads above
 // that RHS evaluation.  Values are stored and re-read unchanged: the arithmetic is the same.
 constexpr int KL_STRIDE = 256;
-__shared__ double kl_buf[4 * 8 * KL_STRIDE];  // 64 KB, allocated only in kernels that use it
+__shared__ double kl_buf[GRT_KL_STAGES * 8 * KL_STRIDE];  // 16 KB per stage, only in kernels that use it
 GDEV void kl_put(int j, const double* k, int D) {
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -465,60 +468,54 @@ GDEV int kl_slot_after(double dep) {
 GDEV double kl_get(int t, int j, int i) { return kl_buf[(j * 8 + i) * KL_STRIDE + t]; }
 
 // QUAD: the Kerr-Schild RHS split over a quad (rhs_ks_quad), `sub` = lane & 3.
-// KLDS: k1..k4 kept in LDS at kl (see kl_put).
-template <int G, bool UNIT_H = false, bool QUAD = false, bool KLDS = false>
+// NKL: stages k1..k_NKL kept in LDS (see kl_put), 0 = none.
+template <int G, bool UNIT_H = false, bool QUAD = false, int NKL = 0>
 GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
                         double* yn, int sub = 0) {
   constexpr int D = Dim<G>::D;
   double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
   int t = 0;  // LDS slot, re-derived after each stage (kl_slot_after)
   // stage j's value k_j[i] (from LDS when parked there)
-#define KV(j, i) (KLDS ? kl_get(t, (j) - 1, (i)) : k##j[i])
+#define KV(j, i) (((j) <= NKL) ? kl_get(t, (j) - 1, (i)) : k##j[i])
   rhs_sel<G, QUAD>(S, rc, y, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k1[i] = UNIT_H ? o[i] : h * o[i];
-  if (KLDS) kl_put(0, k1, D);
+  if (NKL >= 1) kl_put(0, k1, D);
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
   if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k2[i] = UNIT_H ? o[i] : h * o[i];
-  if (KLDS) {
-    kl_put(1, k2, D);
-    t = kl_slot_after(k2[D - 1]);
-  }
+  if (NKL >= 2) kl_put(1, k2, D);
+  if (NKL >= 1) t = kl_slot_after(k2[D - 1]);
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * KV(1, i) + B32 * k2[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k3[i] = UNIT_H ? o[i] : h * o[i];
-  if (KLDS) {
-    kl_put(2, k3, D);
-    t = kl_slot_after(k3[D - 1]);
-  }
+  if (NKL >= 3) kl_put(2, k3, D);
+  if (NKL >= 1) t = kl_slot_after(k3[D - 1]);
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * KV(1, i) + B42 * KV(2, i) + B43 * k3[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k4[i] = UNIT_H ? o[i] : h * o[i];
-  if (KLDS) {
-    kl_put(3, k4, D);
-    t = kl_slot_after(k4[D - 1]);
-  }
+  if (NKL >= 4) kl_put(3, k4, D);
+  if (NKL >= 1) t = kl_slot_after(k4[D - 1]);
 #pragma unroll
   for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * KV(1, i) + B52 * KV(2, i) + B53 * KV(3, i) + B54 * k4[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k5[i] = UNIT_H ? o[i] : h * o[i];
-  if (KLDS) t = kl_slot_after(k5[D - 1]);
+  if (NKL >= 1) t = kl_slot_after(k5[D - 1]);
 #pragma unroll
   for (int i = 0; i < D; ++i)
     tmp[i] = y[i] + B61 * KV(1, i) + B62 * KV(2, i) + B63 * KV(3, i) + B64 * KV(4, i) + B65 * k5[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k6[i] = UNIT_H ? o[i] : h * o[i];
-  if (KLDS) t = kl_slot_after(k6[D - 1]);
+  if (NKL >= 1) t = kl_slot_after(k6[D - 1]);
   double e[8];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
@@ -1258,7 +1255,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
   constexpr bool TAIL = (G == GRT_GEOM_KERR) && !VOL;
   const bool tail_on = TAIL && tl.cap != 0;
-  constexpr bool KLDS = ((GRT_KLDS_GEOMS) >> G) & 1;
+  constexpr int NKL = (((GRT_KLDS_GEOMS) >> G) & 1) ? GRT_KL_STAGES : 0;
   if (tail_on && blockIdx.x == 0 && threadIdx.x == 0) tl.ctl[3] = __builtin_amdgcn_s_memrealtime();
 
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
@@ -1407,8 +1404,8 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
     // (+80 KB of code) is not worth them
     constexpr bool UNIT_H_COPY = GRT_UNIT_H && G != GRT_GEOM_KERR;
     const double err_sq = (UNIT_H_COPY && __ballot(active && h_cur != 1.0) == 0)
-                              ? rkf_attempt<G, UNIT_H_COPY>(S, rc, y, h_cur, yn)
-                              : rkf_attempt<G, false, false, KLDS>(S, rc, y, h_cur, yn);
+                              ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
+                              : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
     n_att++;
     double h_next;
     const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
