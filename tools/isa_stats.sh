@@ -4,9 +4,9 @@ set -e
 ROOT=$(cd $(dirname $0)/.. && pwd)
 W=$(mktemp -d /tmp/isa.XXXX); cd $W
 /opt/rocm/bin/hipcc -I$ROOT/include --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-  -munsafe-fp-atomics --save-temps "$@" -c $ROOT/gr_raytracer_amd/csrc/device/geodesic.hip -o g.o 2>/dev/null
-S=geodesic-hip-amdgcn-amd-amdhsa-gfx950.s
-python3 - "$S" geodesic-hip-amdgcn-amd-amdhsa-gfx950.out <<'PY'
+  -munsafe-fp-atomics --save-temps "$@" -c ${SRC:-$ROOT/gr_raytracer_amd/csrc/device/geodesic.hip} -o g.o 2>/dev/null
+B=$(basename ${SRC:-geodesic.hip} .hip); S=$B-hip-amdgcn-amd-amdhsa-gfx950.s
+python3 - "$S" $B-hip-amdgcn-amd-amdhsa-gfx950.out <<'PY'
 import re, subprocess, sys
 s = open(sys.argv[1]).read()
 syms = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-s", "--wide", sys.argv[2]], capture_output=True, text=True).stdout
