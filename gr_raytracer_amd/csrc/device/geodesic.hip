@@ -96,47 +96,6 @@ GDEV void div2_same_den(double x1, double x2, double y, double* q1, double* q2) 
   *q2 = __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(__builtin_fma(-ds0, m2, n2), fma3, m2, f2), y, x2);
 }
 
-// x[k] / y for N numerators sharing one denominator, each bit-identical to x[k] / y.
-// The compiler's IEEE f64 division is div_scale(x, y, y) (denominator scale), rcp, two
-// Newton steps, div_scale(x, y, x) (numerator scale, with its VCC flag), mul, fma,
-// div_fmas, div_fixup.  Only the denominator scale depends on x, and only when x is zero
-// or extreme (v_div_scale_f64: exp(x) - exp(y) >= 768, or exp(x) <= 53, or y / 1/y
-// denormal).  Under the guard -- y in [2^-100, 2^100] and every |x| in [2^-900, 2^600]
-// (fmax / fmin skip a NaN x: div_fixup returns that NaN on both paths) -- it equals y,
-// so the y-only part (denominator scale, rcp, Newton steps) is computed once.  A lane
-// outside the guard (a tiny non-zero difference: practically never) recomputes each
-// quotient as a plain division; the fallback sits per quotient, which keeps the live
-// ranges short (one if/else around all ten spilled ~120 more registers).
-#ifndef GRT_KS_SHARED_DIV
-#define GRT_KS_SHARED_DIV 1
-#endif
-template <int N>
-GDEV void div_same_den_guarded(const double* x, double y, double* q) {
-  double mx = fabs(x[0]), mn = fabs(x[0]);
-#pragma unroll
-  for (int k = 1; k < N; ++k) {
-    mx = fmax(mx, fabs(x[k]));
-    mn = fmin(mn, fabs(x[k]));
-  }
-  const bool ok = y >= 0x1p-100 && y <= 0x1p100 && mx <= 0x1p600 && mn >= 0x1p-900;
-  bool f0;
-  const double ds = __builtin_amdgcn_div_scale(1.0, y, false, &f0);
-  const double rcp = __builtin_amdgcn_rcp(ds);
-  const double fma0 = __builtin_fma(-ds, rcp, 1.0);
-  const double fma1 = __builtin_fma(rcp, fma0, rcp);
-  const double fma2 = __builtin_fma(-ds, fma1, 1.0);
-  const double fma3 = __builtin_fma(fma1, fma2, fma1);
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    bool fk;
-    const double nk = __builtin_amdgcn_div_scale(x[k], y, true, &fk);
-    const double mk = nk * fma3;
-    double qk = __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(__builtin_fma(-ds, mk, nk), fma3, mk, fk), y, x[k]);
-    if (!ok) qk = x[k] / y;
-    q[k] = qk;
-  }
-}
-
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
 
@@ -287,31 +246,10 @@ GDEV double ks_accel(double radius, double a, int index, double x, double y, dou
   ks_metric(radius, a, x - dx, y - dy, z - dz, mm);
   double two_h = 2.0 * h;
   double D[4][4];
-#if GRT_KS_SHARED_DIV
-  {  // the 10 distinct quotients of the symmetric difference, one shared refinement of 1/2h
-    double num[10], qt[10];
-    int k = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = i; j < 4; ++j) num[k++] = mp[i][j] - mm[i][j];
-    div_same_den_guarded<10>(num, two_h, qt);
-    k = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = i; j < 4; ++j) {
-        D[i][j] = qt[k];
-        D[j][i] = qt[k];
-        k++;
-      }
-  }
-#else
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) D[i][j] = (mp[i][j] - mm[i][j]) / two_h;
-#endif
   double GD[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
