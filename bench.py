@@ -158,16 +158,17 @@ def cpu_baseline(g, workload: str = "c2") -> dict:
 
 
 # ------------------------------------------------------------------- roofline ----
-def find_pmc(workload: str):
+def find_pmc(workload: str, rays: int):
     """The newest PMC summary under profiles/ that measured THIS build's code of the
     workload's integrate kernel (kernel_code_sha256, or the whole device code's hash for
-    summaries that predate it).  Returns (path, summary, note)."""
+    summaries that predate it) on a launch of `rays` rays (per-launch traffic is only
+    comparable between launches of the same size).  Returns (path, summary, note)."""
     from gr_raytracer_amd import _lib as L
 
     kname = PMC_KERNEL[workload]
     mine_k = L.kernel_code_sha256(L.kernel_symbol(kname))
     mine_all = L.device_code_sha256()
-    stale = []
+    stale, other_size = [], []
     for prof in sorted(PMC_DIR.glob("*_pmc.json"), reverse=True):
         try:
             pmc = json.loads(prof.read_text())
@@ -176,8 +177,14 @@ def find_pmc(workload: str):
         if not pmc.get("kernel", "").startswith(kname + ","):
             continue
         if pmc.get("kernel_code_sha256") == mine_k or pmc.get("code_object_sha256") == mine_all:
-            return prof, pmc, None
+            if pmc.get("rays_per_launch") == rays:
+                return prof, pmc, None
+            other_size.append(prof.name)
+            continue
         stale.append(prof.name)
+    if other_size:
+        return None, None, (f"PMC summaries of this build's {kname} ({', '.join(other_size[:3])}) measured launches "
+                            f"of another size than {rays} rays: not used")
     if stale:
         return None, None, f"PMC summaries of {kname} ({', '.join(stale[:3])}) measured another build: not used"
     return None, None, f"no PMC summary of {kname}"
@@ -199,7 +206,7 @@ def roofline(workload: str, geometry: str, accepted: float, attempts: float, ker
            "flop_model": f"{f_att:g}*attempts + {f_step:g}*accepted (SURVEY 8d)",
            "hbm_algorithmic_GBps": n_pixels * BYTES_PER_PIXEL_OUT / (kernel_ms * 1e-3) / 1e9,
            "hbm_peak_GBps": HBM_PEAK_GBS}
-    prof, pmc, note = find_pmc(workload)
+    prof, pmc, note = find_pmc(workload, n_pixels)
     if pmc is None:
         out["traffic_note"] = note
     else:

@@ -130,6 +130,9 @@ def test_roofline_refuses_pmc_of_another_build(grt, tmp_path, monkeypatch):
     # the per-kernel hash of this build's kernel is accepted
     pmc.write_text(json.dumps({"kernel": kname + ", test", "code_object_sha256": "0" * 64,
                                "kernel_code_sha256": grt._lib.kernel_code_sha256(grt._lib.kernel_symbol(kname)),
-                               "hbm_bytes_per_launch": 7.0, "lane_utilisation": 0.9}))
+                               "rays_per_launch": 1000, "hbm_bytes_per_launch": 7.0, "lane_utilisation": 0.9}))
+    # this build's kernel, but a launch of another size: per-launch bytes do not carry over
+    r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 2000, "k")
+    assert r["traffic"] is None and "another size" in r["traffic_note"]
     r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")
     assert r["traffic"] == 7.0 and r["lane_utilisation"] == 0.9

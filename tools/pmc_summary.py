@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 --pmc passes of tools/run_pmc.sh for the integrate kernel.
 
-usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<name>_pmc.json [kernel] [workload text]
+usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<name>_pmc.json [kernel] [workload text] [rays]
 Counter values are summed over the rows of each dispatch of grt::integrate_kernel<1>
 (one C2 frame per dispatch) and reported per launch.  FETCH_SIZE (KB) is doubled per
 the gfx950 correction in MI355X_MICROARCH.md; WRITE_SIZE (KB) is taken as is.
@@ -17,6 +17,7 @@ from gr_raytracer_amd._lib import device_code_sha256, kernel_code_sha256, kernel
 
 KERNEL = sys.argv[3] if len(sys.argv) > 3 else "grt::integrate_kernel<1, false>"
 WORKLOAD = sys.argv[4] if len(sys.argv) > 4 else "one frame of tools/prof_target.py c2 (1500x1500, 2.25M rays)"
+RAYS = int(sys.argv[5]) if len(sys.argv) > 5 else 2250000  # rays per launch of the profiled workload
 
 
 def load(pass_dir):
@@ -48,6 +49,7 @@ def main():
     write_b = counters.get("WRITE_SIZE", 0.0) * 1024
     out = {
         "kernel": f"{KERNEL}, {WORKLOAD}",
+        "rays_per_launch": RAYS,  # bench.py uses the traffic only for a launch of this size
         # the device code the passes measured: bench.py refuses a summary of another build
         "code_object_sha256": device_code_sha256(),
         # this kernel's own code + descriptor (PC-relative displacements masked): stays
