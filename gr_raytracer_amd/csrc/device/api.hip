@@ -446,7 +446,7 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
 int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList* tl, int* tail_blocks) {
   std::memset(tl, 0, sizeof(*tl));
   *tail_blocks = 0;
-  if (s->desc.geometry != GRT_GEOM_KERR || dc.vol || g_tail == 0) return 0;
+  if (s->desc.geometry != GRT_GEOM_KERR || g_tail == 0) return 0;
   const int blocks = dc.cus * GRT_TAIL_WAVES;
   const uint64_t threshold = g_tail > 0 ? (uint64_t)g_tail : (uint64_t)blocks * grt::TAIL_RAYS_PER_BLOCK;
   const uint64_t cap = lanes;

@@ -1253,7 +1253,7 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   const uint64_t n = ws.n;
   // items present: the capacity, or the count the adaptive pass decided on the device
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
-  constexpr bool TAIL = (G == GRT_GEOM_KERR) && !VOL;
+  constexpr bool TAIL = (G == GRT_GEOM_KERR);
   const bool tail_on = TAIL && tl.cap != 0;
   constexpr int NKL = (((GRT_KLDS_GEOMS) >> G) & 1) ? GRT_KL_STAGES : 0;
   if (tail_on && blockIdx.x == 0 && threadIdx.x == 0) tl.ctl[3] = __builtin_amdgcn_s_memrealtime();
@@ -1493,8 +1493,8 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
           rc.e = ws.rc[1 * n + s.idx];
           rc.lz = ws.rc[2 * n + s.idx];
           rc.q = ws.rc[3 * n + s.idx];
-          rc.pt = 0.0;
-          rc.pphi = 0.0;
+          rc.pt = VOL ? ws.rc[4 * n + s.idx] : 0.0;
+          rc.pphi = VOL ? ws.rc[5 * n + s.idx] : 0.0;
           active = true;
         }
       }
@@ -2103,15 +2103,16 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
 }
 
 // ------------------------------------------------------------------ launch -------
-// Plain scenes: integrate [-> tail] -> shade.  Volumetric scenes: integrate -> gather
-// raymarch jobs -> march (persistent, lane refill) -> composite; ws.march must be zeroed.
+// Plain scenes: integrate [-> tail] -> shade.  Volumetric scenes: integrate [-> tail] ->
+// gather raymarch jobs -> march (persistent, lane refill) -> composite; ws.march must be
+// zeroed.  The tail (Kerr-Schild) continues the long rays the integrate kernel handed off.
 template <int G>
 static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
                            unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
                            bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream) {
   const unsigned nb = (unsigned)((ws.n + 255) / 256);
   TailList tl = tl_in;
-  if (G != GRT_GEOM_KERR || vol || tail_blocks <= 0) tl.cap = 0;
+  if (G != GRT_GEOM_KERR || tail_blocks <= 0) tl.cap = 0;
   if (!vol) {
     hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
                        d_counter, d_stats, tl);
@@ -2132,6 +2133,12 @@ static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Wo
                      d_counter, d_stats, tl);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if constexpr (G == GRT_GEOM_KERR) {
+    if (tl.cap) {
+      hipLaunchKernelGGL((tail_kernel<G, true>), dim3(tail_blocks), dim3(256), 0, stream, d_scene, ws, tl, d_stats);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+  }
   hipLaunchKernelGGL((shade_kernel<G, 1>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL((march_kernel<G>), dim3(blocks), dim3(256), 0, stream, d_scene, ws);

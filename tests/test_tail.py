@@ -52,3 +52,30 @@ def test_tail_hand_off_is_bit_identical(grt, gpu, rect):
             assert got.stats["rays"] == base.stats["rays"]
     finally:
         _set_tail(grt, -1)
+
+
+@pytest.mark.gpu
+def test_tail_hand_off_is_bit_identical_volumetric(grt, gpu):
+    """kerr-volumetric-stony.toml (Kerr-Schild + VolumetricDisc) with C4's camera: the
+    handed-off rays keep their volumetric window records (chord directions, frequency
+    data), so the raymarch jobs, samples and the composited frame are unchanged."""
+    hs = host_scene(grt, "kerr-volumetric-stony.toml", c4_opts(grt, width=128, height=128, max_steps=100000))
+    sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
+    rect = (0, 0, 128, 128)
+    try:
+        _set_tail(grt, 0)
+        base, n0 = _render(grt, sc, rect)
+        assert n0 == 0
+        assert base.steps.max() > 50000 and base.stats["march_jobs"] > 0
+        for mode in (-1, 1 << 40, 37):
+            _set_tail(grt, mode)
+            got, handed = _render(grt, sc, rect)
+            assert handed > 0, mode
+            assert np.array_equal(got.xyza64, base.xyza64), mode
+            for f in ("ray_class", "status", "steps", "stop_reason"):
+                assert np.array_equal(getattr(got, f), getattr(base, f)), (mode, f)
+            for k in ("accepted_steps", "attempts", "rays", "march_jobs", "march_samples", "march_noise_samples",
+                      "march_emit_samples"):
+                assert got.stats[k] == base.stats[k], (mode, k)
+    finally:
+        _set_tail(grt, -1)
