@@ -1,11 +1,14 @@
 """Kerr-Schild frames at the reference's example size (docs/example-render-commands.md:
 1000x1000, camera -10,0,-0.5, theta 1.52, psi -1.57, max-steps 1e6): kerr.toml and the
-volumetric kerr-volumetric-stony.toml, one timed frame each (after a small warm-up)."""
+volumetric kerr-volumetric-stony.toml, one timed frame each (after a small warm-up), with
+the long-ray hand-off timeline and the step-count tail of the frame."""
 import json
 import os
 import sys
 import time
 from pathlib import Path
+
+import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
@@ -21,9 +24,18 @@ for name in sys.argv[2:] or ["kerr.toml", "kerr-volumetric-stony.toml"]:
     sc = g.Scene(hs.desc_ptr(), keepalive=hs)
     sc.render_pixels(0, 0, 16, 16, aux=False)
     t0 = time.perf_counter()
-    r = sc.render_pixels(aux=False)
+    r = sc.render_pixels(aux=True)
+    wall = time.perf_counter() - t0
     st = r.stats
-    print(json.dumps({"scene": name, "pixels": size * size, "wall_s": round(time.perf_counter() - t0, 3),
-                      "kernel_ms": st["kernel_ms"], "accepted_steps": st["accepted_steps"],
-                      "march_jobs": st["march_jobs"], "march_samples": st["march_samples"],
-                      "tail": os.environ.get("GRT_TAIL", "auto"), "handoffs": sc.tail_handoffs()}), flush=True)
+    rep = sc.tail_report(capacity=1 << 20)
+    tl = {k: round(rep[k], 3) for k in ("drained_s", "handoff_s", "tail_end_s")}
+    steps = r.steps.astype(np.int64)
+    if rep["handed_off"]:
+        rem = steps[rep["slot"].astype(np.int64)] - rep["step"].astype(np.int64)
+        tl.update(max_remaining=int(rem.max()), longest_at_handoff=int(rep["step"][int(rem.argmax())]))
+    print(json.dumps({"scene": name, "pixels": size * size, "wall_s": round(wall, 3), "kernel_ms": st["kernel_ms"],
+                      "accepted_steps": st["accepted_steps"], "march_jobs": st["march_jobs"],
+                      "march_samples": st["march_samples"], "tail": os.environ.get("GRT_TAIL", "auto"),
+                      "handoffs": int(rep["handed_off"]), "timeline": tl,
+                      "rays_over": {str(k): int((steps > k).sum()) for k in (100000, 300000, 500000, 900000)},
+                      "max_steps_rays": int((steps >= 999999).sum())}), flush=True)
