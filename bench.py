@@ -220,6 +220,23 @@ def roofline(workload: str, geometry: str, accepted: float, attempts: float, ker
 
 
 # ------------------------------------------------------------------ workloads ----
+def reduce_over_ranks(elapsed: float, accepted: float, attempts: float, world: int, device="cpu"):
+    """The weak-scaling line's job totals: the max over ranks of the timed region and the
+    sums of every rank's accepted steps and attempts (backend-agnostic: RCCL on the GPUs,
+    gloo in tests)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([elapsed, float(accepted), float(attempts)], dtype=torch.float64, device=device)
+    if world > 1:
+        tmax = t[:1].clone()
+        steps = t[1:].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(steps, op=dist.ReduceOp.SUM)
+        return float(tmax[0]), float(steps[0]), float(steps[1])
+    return float(t[0]), float(t[1]), float(t[2])
+
+
 def run_c2(args, rank, world, local_rank, dev):
     import torch
     import torch.distributed as dist
@@ -271,13 +288,7 @@ def run_c2(args, rank, world, local_rank, dev):
     counters = stats.cpu().tolist()  # accepted, attempts, rays, overflows (summed over K frames)
     accepted, attempts = counters[0], counters[1]
 
-    t = torch.tensor([elapsed, float(accepted), float(attempts)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-    total_acc, total_att = float(t[1]), float(t[2])
+    elapsed, total_acc, total_att = reduce_over_ranks(elapsed, accepted, attempts, world, dev)
     if rank != 0:
         return None
     line = {

@@ -136,3 +136,33 @@ def test_roofline_refuses_pmc_of_another_build(grt, tmp_path, monkeypatch):
     assert r["traffic"] is None and "another size" in r["traffic_note"]
     r = bench.roofline("c2", "schwarzschild", 1e9, 1e9, 100.0, 1000, "k")
     assert r["traffic"] == 7.0 and r["lane_utilisation"] == 0.9
+
+
+def _reduce_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = bench.reduce_over_ranks(1.0 + rank, 100.0 * (rank + 1), 101.0 * (rank + 1), world)
+        with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+            json.dump(r, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_weak_scaling_totals_gloo_world2():
+    """bench.reduce_over_ranks (the C2 weak-scaling line): max over ranks of the timed
+    region, sums of the steps, identical on every rank."""
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_reduce_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        got = [json.load(open(os.path.join(d, f"r{r}.json"))) for r in range(2)]
+    assert got[0] == got[1] == [2.0, 300.0, 303.0]
+    import bench
+
+    assert list(bench.reduce_over_ranks(1.5, 7.0, 8.0, 1)) == [1.5, 7.0, 8.0]
