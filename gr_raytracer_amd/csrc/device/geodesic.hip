@@ -46,6 +46,9 @@ namespace grt {
 #ifndef GRT_KLDS_GEOMS
 #define GRT_KLDS_GEOMS (1 << GRT_GEOM_KERR)  // integrate kernels whose RKF stages k1..k4 live in LDS
 #endif
+#ifndef GRT_LONG_PRIO
+#define GRT_LONG_PRIO 0  // Kerr-Schild: issue priority for waves holding a ray past this many steps (0 = off)
+#endif
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
@@ -1262,6 +1265,8 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
   bool active = false, done = false;
   bool started = false, ended = false;  // since the last live-count update (tail_on)
   uint32_t poll = 0;
+  bool prio_high = false;  // GRT_LONG_PRIO: this wave's s_setprio level (wave-uniform)
+  (void)prio_high;
   uint64_t idx = 0;      // output slot of the current ray
   double y[8];           // state
   double c[3];           // Cartesian position of the last accepted step (when c_valid)
@@ -1396,6 +1401,18 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
       }
     }
     if (__ballot(!done) == 0) break;
+#if GRT_LONG_PRIO
+    if constexpr (TAIL) {
+      // waves that carry a long ray (past GRT_LONG_PRIO accepted steps) take VALU issue
+      // priority over their SIMD partner: the frame ends on those rays, not on the others
+      const bool long_wave = __ballot(active && i > (uint64_t)GRT_LONG_PRIO) != 0;
+      if (long_wave != prio_high) {
+        if (long_wave) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+        prio_high = long_wave;
+      }
+    }
+#endif
     if (!active) continue;
 
     // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
