@@ -470,11 +470,142 @@ GDEV int kl_slot_after(double dep) {
 }
 GDEV double kl_get(int t, int j, int i) { return kl_buf[(j * 8 + i) * KL_STRIDE + t]; }
 
+// State components the RHS reads (the others -- t, and phi where the metric does not
+// depend on it -- only receive stage values, so their stage inputs are never formed).
+template <int G>
+GDEV constexpr bool rhs_reads(int i) {
+  if (G == GRT_GEOM_EUCLIDEAN) return i >= 4;
+  if (G == GRT_GEOM_KERR) return i >= 1;
+  return i == 1 || i == 2 || i >= 4;  // Schwarzschild, EuclideanSpherical, KerrBL: r, theta, velocities
+}
+
+// nalgebra norm(): 8-accumulator unrolled dot, ((a0+a4) + (a1+a5)) + (a2+a6) + (a3+a7)
+template <int D>
+GDEV double err_norm_sq(const double* e) {
+  double res;
+  if constexpr (D == 8) {
+    res = e[0] * e[0] + e[4] * e[4];
+    res += e[1] * e[1] + e[5] * e[5];
+    res += e[2] * e[2] + e[6] * e[6];
+    res += e[3] * e[3] + e[7] * e[7];
+  } else {
+    res = e[0] * e[0] + e[4] * e[4];
+    res += e[1] * e[1] + e[5] * e[5];
+    res += e[2] * e[2];
+    res += e[3] * e[3];
+  }
+  return res;
+}
+
+#ifndef GRT_RK_FOLD
+#define GRT_RK_FOLD 1  // running RKF sums (rkf_attempt_fold) for every chart but Kerr-Schild
+#endif
+
+// rkf45_step with every left-to-right sum of runge_kutta.rs:94-124 evaluated as a running
+// sum as soon as its terms exist.  The sums are the reference's, term by term in the same
+// order ((y + B61*k1) + B62*k2) + ..., so every value is bit-identical to rkf_attempt_full;
+// what changes is how many stage values are live across an RHS evaluation:
+//   - a component the RHS does not read (rhs_reads) folds k_j into y_new and the error
+//     right away: 2 live values instead of up to 6;
+//   - the others keep k1..k3 until k4 exists, then fold k1..k4 into the stage-5 input, the
+//     stage-6 partial, y_new and the error: 3 live values across RHS 5 and 2 across RHS 6,
+//     instead of 4 and 5.
+template <int G, bool UNIT_H, bool QUAD, int NKL>
+GDEV double rkf_attempt_fold(const DevScene& S, const RayConst& rc, const double* y, double h, double* yn,
+                             int sub) {
+  constexpr int D = Dim<G>::D;
+  double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8], p6[8], e[8];
+  int t = 0;  // LDS slot, re-derived after each stage (kl_slot_after)
+#define KV(j, i) (((j) <= NKL) ? kl_get(t, (j) - 1, (i)) : k##j[i])
+#define STAGE(kj)                                                   \
+  _Pragma("unroll") for (int i = 0; i < D; ++i) kj[i] = UNIT_H ? o[i] : h * o[i];
+  rhs_sel<G, QUAD>(S, rc, y, o, sub);
+  STAGE(k1)
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (!rhs_reads<G>(i)) {
+      yn[i] = y[i] + CH1 * k1[i];
+      e[i] = CT1 * k1[i];
+    }
+  if (NKL >= 1) kl_put(0, k1, D);
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
+  if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
+  STAGE(k2)
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (!rhs_reads<G>(i)) {
+      yn[i] = yn[i] + CH2 * k2[i];
+      e[i] = e[i] + CT2 * k2[i];
+    }
+  if (NKL >= 2) kl_put(1, k2, D);
+  if (NKL >= 1) t = kl_slot_after(k2[D - 1]);
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * KV(1, i) + B32 * k2[i];
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
+  STAGE(k3)
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (!rhs_reads<G>(i)) {
+      yn[i] = yn[i] + CH3 * k3[i];
+      e[i] = e[i] + CT3 * k3[i];
+    }
+  if (NKL >= 3) kl_put(2, k3, D);
+  if (NKL >= 1) t = kl_slot_after(k3[D - 1]);
+#pragma unroll
+  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * KV(1, i) + B42 * KV(2, i) + B43 * k3[i];
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
+  STAGE(k4)
+  if (NKL >= 1) t = kl_slot_after(k4[D - 1]);
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    if (!rhs_reads<G>(i)) {
+      yn[i] = yn[i] + CH4 * k4[i];
+      e[i] = e[i] + CT4 * k4[i];
+    } else {
+      const double a1 = KV(1, i), a2 = KV(2, i), a3 = KV(3, i), a4 = k4[i];
+      tmp[i] = y[i] + B51 * a1 + B52 * a2 + B53 * a3 + B54 * a4;
+      p6[i] = y[i] + B61 * a1 + B62 * a2 + B63 * a3 + B64 * a4;
+      yn[i] = y[i] + CH1 * a1 + CH2 * a2 + CH3 * a3 + CH4 * a4;
+      e[i] = CT1 * a1 + CT2 * a2 + CT3 * a3 + CT4 * a4;
+    }
+  }
+  if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
+  STAGE(k5)
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    if (rhs_reads<G>(i)) tmp[i] = p6[i] + B65 * k5[i];
+    yn[i] = yn[i] + CH5 * k5[i];
+    e[i] = e[i] + CT5 * k5[i];
+  }
+  rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
+  STAGE(k6)
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    yn[i] = yn[i] + CH6 * k6[i];
+    e[i] = e[i] + CT6 * k6[i];
+  }
+#undef STAGE
+#undef KV
+  if (D < 8) {
+    yn[6] = 0.0;
+    yn[7] = 0.0;
+  }
+  return err_norm_sq<D>(e);
+}
+
 // QUAD: the Kerr-Schild RHS split over a quad (rhs_ks_quad), `sub` = lane & 3.
 // NKL: stages k1..k_NKL kept in LDS (see kl_put), 0 = none.
 template <int G, bool UNIT_H = false, bool QUAD = false, int NKL = 0>
 GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, double h,
                         double* yn, int sub = 0) {
+  // Kerr-Schild keeps the plain form: its stages k1..k4 sit in LDS (NKL), which frees
+  // more registers than the running sums (measured: 17 -> 122 spilled VGPRs with them)
+  if constexpr (GRT_RK_FOLD && G != GRT_GEOM_KERR) {
+    return rkf_attempt_fold<G, UNIT_H, QUAD, NKL>(S, rc, y, h, yn, sub);
+  }
   constexpr int D = Dim<G>::D;
   double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
   int t = 0;  // LDS slot, re-derived after each stage (kl_slot_after)
@@ -531,20 +662,7 @@ GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, 
     yn[6] = 0.0;
     yn[7] = 0.0;
   }
-  // nalgebra norm(): 8-accumulator unrolled dot, ((a0+a4) + (a1+a5)) + (a2+a6) + (a3+a7)
-  double res;
-  if constexpr (D == 8) {
-    res = e[0] * e[0] + e[4] * e[4];
-    res += e[1] * e[1] + e[5] * e[5];
-    res += e[2] * e[2] + e[6] * e[6];
-    res += e[3] * e[3] + e[7] * e[7];
-  } else {
-    res = e[0] * e[0] + e[4] * e[4];
-    res += e[1] * e[1] + e[5] * e[5];
-    res += e[2] * e[2];
-    res += e[3] * e[3];
-  }
-  return res;
+  return err_norm_sq<D>(e);
 }
 
 // ---- chart helpers ----

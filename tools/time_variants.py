@@ -1,9 +1,15 @@
-"""Time the C2 frame with each experimental libgrt variant (one subprocess each)."""
-import json, os, subprocess, sys
+"""Time the C2 (and C3) frame with each experimental libgrt build in variants/<name>/
+(tools/build_variant.sh), one subprocess per variant and config, in the order given on
+the command line (repeat names to alternate).  Frames must be identical (md5)."""
+import json
+import os
+import subprocess
+import sys
 from pathlib import Path
+
 ROOT = Path(__file__).resolve().parents[1]
 CODE = r'''
-import sys, time, json
+import sys, json, hashlib
 sys.path.insert(0, "%s")
 import gr_raytracer_amd as g
 if "C3" in sys.argv:
@@ -13,23 +19,23 @@ else:
     opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, max_steps=100000)
     hs = g.HostScene("%s/tests/golden/scenes/schwarzschild.toml", opts, "%s/tests/golden")
 sc = g.Scene(hs.desc_ptr(), keepalive=hs)
-best = None
-for i in range(2):
+ms = []
+for i in range(3):
     r = sc.render_pixels(0, 0, 1500, 1500, aux=False)
-    st = r.stats
-    if best is None or st["kernel_ms"] < best["kernel_ms"]:
-        best = st
-import hashlib
-best["md5"] = hashlib.md5(r.xyza.tobytes()).hexdigest()[:12]
-print(json.dumps(best))
+    ms.append(r.stats["kernel_ms"])
+st = r.stats
+st["ms"] = ms
+st["md5"] = hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12]
+print(json.dumps(st))
 ''' % ((ROOT,) * 5)
+configs = os.environ.get("CONFIGS", "C2,C3").split(",")
 for name in sys.argv[1:]:
-  for cfg in ("C2", "C3"):
-    env = dict(os.environ, GRT_LIB=str(ROOT / "variants" / name / "libgrt.so"), GRT_LIB_ALLOW_MISSING="1")
-    out = subprocess.run([sys.executable, "-c", CODE, cfg], env=env, capture_output=True, text=True, timeout=600)
-    if out.returncode != 0:
-        print(name, "FAILED", out.stderr[-2000:], flush=True)
-        sys.exit(1)
-    st = json.loads(out.stdout.strip().splitlines()[-1])
-    print(f"{name:16s} {cfg} kernel {st['kernel_ms']:9.1f} ms  steps/s {st['accepted_steps']/st['kernel_ms']*1e3:.3e} "
-          f"attempts {st['attempts']} frame-md5 {st['md5']}", flush=True)
+    for cfg in configs:
+        env = dict(os.environ, GRT_LIB=str(ROOT / "variants" / name / "libgrt.so"))
+        out = subprocess.run([sys.executable, "-c", CODE, cfg], env=env, capture_output=True, text=True, timeout=300)
+        if out.returncode != 0:
+            print(name, "FAILED", out.stderr[-2000:], flush=True)
+            sys.exit(1)
+        st = json.loads(out.stdout.strip().splitlines()[-1])
+        print(json.dumps({"variant": name, "config": cfg, "kernel_ms": [round(x, 1) for x in st["ms"]],
+                          "accepted": st["accepted_steps"], "attempts": st["attempts"], "md5": st["md5"]}), flush=True)
