@@ -49,6 +49,9 @@ namespace grt {
 #ifndef GRT_LONG_PRIO
 #define GRT_LONG_PRIO 0  // Kerr-Schild: issue priority for waves holding a ray past this many steps (0 = off)
 #endif
+#ifndef GRT_SINCOS_B
+#define GRT_SINCOS_B 1  // Schwarzschild / KerrBL RHS: wave-uniform straight-line sincos (region B)
+#endif
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
@@ -301,6 +304,34 @@ GDEV void metric_bl(double r_s, double a, double r, double sin_t, double cos_t, 
   g[3][0] = g_tph;
 }
 
+// sincos(theta), then body(sin, cos, fast).  When every lane of the wave is in one of
+// sincos's region-B cases (x near pi/2; glibc_math.h sincos_b_*), the sincos is the
+// straight-line form of that case and body runs in the same basic block, so its own
+// dependency chains (the divisions) interleave with the sincos polynomial; fast = true
+// there (the caller passes fast_ok = whether body may then take its fast form).  The same
+// bits as rsincos in every case (tests/test_glibc_math.py).
+template <class F>
+GDEV void with_sincos(double theta, bool fast_ok, F&& body) {
+#if GRT_SINCOS_B
+  if (fast_ok) {
+    double st, ct;
+    if (__ballot(!glibc::sincos_b_table_ok(theta)) == 0) {
+      glibc::sincos_b_table(theta, &st, &ct);
+      body(st, ct, true);
+      return;
+    }
+    if (__ballot(!glibc::sincos_b_taylor_ok(theta)) == 0) {
+      glibc::sincos_b_taylor(theta, &st, &ct);
+      body(st, ct, true);
+      return;
+    }
+  }
+#endif
+  double st, ct;
+  rsincos(theta, &st, &ct);
+  body(st, ct, false);
+}
+
 // ---- the ODE right-hand sides ----
 template <int G>
 GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o) {
@@ -308,30 +339,32 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     double radius = S.radius;
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
-    double st, ct;
-    rsincos(theta, &st, &ct);
-    double radius_over_r, two_over_r;
+    auto body = [&](double st, double ct, bool fast) {
+      double radius_over_r, two_over_r;
 #if GRT_SHARED_DIV
-    if (S.div_share) {
-      div2_same_den(radius, 2.0, r, &radius_over_r, &two_over_r);
-    } else
+      if (fast || S.div_share) {
+        div2_same_den(radius, 2.0, r, &radius_over_r, &two_over_r);
+      } else
 #endif
-    {
-      radius_over_r = radius / r;
-      two_over_r = 2.0 / r;
-    }
-    double a = 1.0 - radius_over_r;
-    double a_prime = radius / (r * r);
-    double aprime_over_a = a_prime / a;
-    o[0] = v_t;
-    o[1] = v_r;
-    o[2] = v_theta;
-    o[3] = v_phi;
-    o[4] = -(aprime_over_a)*v_t * v_r;
-    o[5] = -0.5 * a * a_prime * v_t * v_t + 0.5 * (aprime_over_a)*v_r * v_r +
-           a * r * (v_theta * v_theta + v_phi * v_phi * st * st);
-    o[6] = -(two_over_r)*v_r * v_theta + st * ct * v_phi * v_phi;
-    o[7] = -(two_over_r)*v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
+      {
+        radius_over_r = radius / r;
+        two_over_r = 2.0 / r;
+      }
+      double a = 1.0 - radius_over_r;
+      double a_prime = radius / (r * r);
+      double aprime_over_a = a_prime / a;
+      o[0] = v_t;
+      o[1] = v_r;
+      o[2] = v_theta;
+      o[3] = v_phi;
+      o[4] = -(aprime_over_a)*v_t * v_r;
+      o[5] = -0.5 * a * a_prime * v_t * v_t + 0.5 * (aprime_over_a)*v_r * v_r +
+             a * r * (v_theta * v_theta + v_phi * v_phi * st * st);
+      o[6] = -(two_over_r)*v_r * v_theta + st * ct * v_phi * v_phi;
+      o[7] = -(two_over_r)*v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
+    };
+    // fast form: the shared reciprocal, decided with the wave-uniform case (S.div_share)
+    with_sincos(theta, S.div_share, body);
   } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:48-70
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
@@ -348,22 +381,22 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
   } else if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:141-174
     double radius = S.radius, a = S.a, e = rc.e, l_z = rc.lz, q = rc.q;
     double r = y[1], theta = y[2];
-    double st, ct;
-    rsincos(theta, &st, &ct);
-    double del = bl_delta(r, radius, a);
-    double r2a2 = r * r + a * a;
-    double p_r = r2a2 * e - a * l_z;
-    double sin2 = st * st;
-    o[0] = r2a2 / del * p_r + a * (l_z - a * e * sin2);
-    o[1] = y[4];
-    o[2] = y[5];
-    o[3] = a / del * p_r + l_z / sin2 - a * e;
-    double le = l_z - a * e;
-    double carter = le * le + q;
-    o[4] = (4.0 * r * e * p_r - (2.0 * r - radius) * carter) / 2.0;
-    o[5] = (-2.0 * a * a * e * e * ct * st + 2.0 * l_z * l_z * ct / (st * (st * st))) / 2.0;
-    o[6] = 0.0;
-    o[7] = 0.0;
+    with_sincos(theta, true, [&](double st, double ct, bool) {
+      double del = bl_delta(r, radius, a);
+      double r2a2 = r * r + a * a;
+      double p_r = r2a2 * e - a * l_z;
+      double sin2 = st * st;
+      o[0] = r2a2 / del * p_r + a * (l_z - a * e * sin2);
+      o[1] = y[4];
+      o[2] = y[5];
+      o[3] = a / del * p_r + l_z / sin2 - a * e;
+      double le = l_z - a * e;
+      double carter = le * le + q;
+      o[4] = (4.0 * r * e * p_r - (2.0 * r - radius) * carter) / 2.0;
+      o[5] = (-2.0 * a * a * e * e * ct * st + 2.0 * l_z * l_z * ct / (st * (st * st))) / 2.0;
+      o[6] = 0.0;
+      o[7] = 0.0;
+    });
   } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:200-241
     double radius = S.radius, a = S.a;
     double x = y[1], yy = y[2], z = y[3];

@@ -410,6 +410,49 @@ GRT_GLIBC_FN bool sincos_fast(double x, double* sinx, double* cosx) {
   return false;
 }
 
+// The commonest case of sincos_fast for a polar angle near the equator, as straight-line
+// code: region B (0.855469 <= |x| < 2.426265, where sin x = +-do_cos(pi/2 - |x|) and
+// cos x = do_sin(a, da)) with do_sin's table path (|a| >= TAYLOR_MAX).  sincos_b_table_ok
+// says whether x is in that case; sincos_b_table then returns sincos_fast's bits.
+GRT_GLIBC_FN bool sincos_b_table_ok(double x) {
+  const uint32_t k = (uint32_t)(as_u64(x) >> 32) & 0x7fffffffu;
+  const double y = HP0 - fabs_(x);
+  const double a = y + HP1;
+  return k >= 0x3feb6000u && k < 0x400368fdu && !(fabs_(a) < TAYLOR_MAX);
+}
+GRT_GLIBC_FN void sincos_b_table(double x, double* sinx, double* cosx) {
+  const double y = HP0 - fabs_(x);
+  const double a = y + HP1;
+  double da = (y - a) + HP1;
+  *sinx = copysign_(do_cos_nf(y, HP1), x);
+  // do_sin_nf(a, da) past its Taylor branch
+  if (a <= 0.0) da = -da;
+  const double u = BIG + fabs_(a);
+  const double xr = fabs_(a) - (u - BIG);
+  const int k = (int)((uint32_t)as_u64(u) << 2);
+  const double sn = GRT_SINCOS(k), ssn = GRT_SINCOS(k + 1), cs = GRT_SINCOS(k + 2), ccs = GRT_SINCOS(k + 3);
+  const double xx = xr * xr;
+  const double s = xr + (da + xr * xx * (SN3 + xx * SN5));
+  const double c = xr * da + xx * (CS2 + xx * (CS4 + xx * CS6));
+  const double cor = (ssn + s * ccs - sn * c) + cs * s;
+  *cosx = copysign_(sn + cor, a);
+}
+
+// Region B with do_sin's Taylor branch (|a| < TAYLOR_MAX: x within ~7 degrees of pi/2).
+GRT_GLIBC_FN bool sincos_b_taylor_ok(double x) {
+  const uint32_t k = (uint32_t)(as_u64(x) >> 32) & 0x7fffffffu;
+  const double y = HP0 - fabs_(x);
+  const double a = y + HP1;
+  return k >= 0x3feb6000u && k < 0x400368fdu && fabs_(a) < TAYLOR_MAX;
+}
+GRT_GLIBC_FN void sincos_b_taylor(double x, double* sinx, double* cosx) {
+  const double y = HP0 - fabs_(x);
+  const double a = y + HP1;
+  const double da = (y - a) + HP1;
+  *sinx = copysign_(do_cos_nf(y, HP1), x);
+  *cosx = taylor_sin_nf(a, da);
+}
+
 // sincos_fast without the region branches, for angles spread over (-pi, pi] within a
 // wave (the VolumetricDisc's in-plane angle): every region of sincos_fast evaluates one
 // do_sin_nf and one do_cos_nf, so the arguments are selected per lane, both are

@@ -1,4 +1,5 @@
-// Host build of glibc_math.h's sincos_fast checked against glibc sincos, bit for bit.
+// Host build of glibc_math.h's sincos_fast (and its branch-free and region-B forms)
+// checked against glibc sincos, bit for bit.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -22,6 +23,7 @@ int main(int argc, char** argv) {
       case 1: x = (u01(rng) - 0.5) * 40.0; break;
       case 2: x = std::ldexp(u01(rng) - 0.5, (int)(rng() % 60) - 40); break;
       case 3: x = 1.5707963267948966 + (u01(rng) - 0.5) * 1e-6; break;
+      case 6: x = 1.5707963267948966 + (u01(rng) - 0.5) * 0.3; break;  // both sides of TAYLOR_MAX
       case 5: x = (u01(rng) * 2.0 - 1.0) * 3.141592653589793; break;  // VolumetricDisc phi
       default: x = (u01(rng) - 0.5) * 2e8;
     }
@@ -31,8 +33,12 @@ int main(int argc, char** argv) {
     sincos(x, &ws, &wc);
     // the branch-free variant must return the same bits on the same domain
     const bool uok = grt::glibc::sincos_fast_uniform(x, &us, &uc);
+    // and so must the straight-line region-B form wherever it claims the case
+    double bs = ws, bc = wc;
+    if (grt::glibc::sincos_b_table_ok(x)) grt::glibc::sincos_b_table(x, &bs, &bc);
+    if (grt::glibc::sincos_b_taylor_ok(x)) grt::glibc::sincos_b_taylor(x, &bs, &bc);
     if (memcmp(&gs, &ws, 8) != 0 || memcmp(&gc, &wc, 8) != 0 || !uok || memcmp(&us, &ws, 8) != 0 ||
-        memcmp(&uc, &wc, 8) != 0) {
+        memcmp(&uc, &wc, 8) != 0 || memcmp(&bs, &ws, 8) != 0 || memcmp(&bc, &wc, 8) != 0) {
       if (bad < 5) printf("# mismatch x=%a got=(%a,%a) uniform=(%a,%a) want=(%a,%a)\n", x, gs, gc, us, uc, ws, wc);
       ++bad;
     }

@@ -41,7 +41,8 @@ def test_tables_match_the_installed_libm():
 
 
 TRIG_MODES = {0: "ray theta", 1: "several periods", 2: "magnitudes 2^-41..2^19", 3: "near pi/2",
-              4: "up to the reduction limit", 5: "(-pi, pi): VolumetricDisc phi"}
+              4: "up to the reduction limit", 5: "(-pi, pi): VolumetricDisc phi",
+              6: "pi/2 +- 0.15 (region B, Taylor and table)"}
 
 
 def _build(tmp_path_factory, name, extra=()):
