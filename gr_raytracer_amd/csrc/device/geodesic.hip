@@ -52,6 +52,9 @@ namespace grt {
 #ifndef GRT_SINCOS_B
 #define GRT_SINCOS_B 1  // Schwarzschild / KerrBL RHS: wave-uniform straight-line sincos (region B)
 #endif
+#ifndef GRT_QUICK_STEP
+#define GRT_QUICK_STEP 1  // Schwarzschild: the far-field accepted step as one straight-line block
+#endif
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
@@ -1237,6 +1240,36 @@ GDEV bool window_far(const DevScene& S, const double* ya, const double* yb) {
   }
 }
 
+// The commonest accepted step of a curvilinear chart as one predicate, evaluated without
+// branches over the lanes (integrate_kernel's quick step): step_control's first case
+// (err_sq < tiny_err_sq: accepted, next h = clamp(4h)), window_far for every object (no
+// chord test, c_valid = false) and should_stop's checks all passing on yn with the
+// celestial test decided by r (finite, outside the horizon, inside the celestial shell,
+// not the last step).  True only where the general path does exactly the quick step's
+// updates; every other case takes the general path.
+template <int G>
+GDEV bool quick_step_ok(const DevScene& S, double err_sq, const double* y, const double* yn, uint64_t i_next) {
+  static_assert(G == GRT_GEOM_SCHWARZSCHILD, "quick step: Schwarzschild only");
+  constexpr double N_LO = -1.5707963257948966, N_HI = 1.5707963257948966;
+  constexpr double S_LO = 1.5707963277948966, S_HI = 4.7123889793846899;
+  const double ra = y[1], rb = yn[1], ta = y[2], tb = yn[2];
+  bool ok = (err_sq < S.tiny_err_sq) & (S.far_ok != 0);
+  const bool north = (ta > N_LO) & (ta < N_HI) & (tb > N_LO) & (tb < N_HI);
+  const bool south = (ta > S_LO) & (ta < S_HI) & (tb > S_LO) & (tb < S_HI);
+  const bool ratio = (ra >= 1e-3 * rb) & (rb >= 1e-3 * ra) & (ra > 0.0);
+  for (uint32_t k = 0; k < S.n_objects; ++k) {
+    const DevObject& o = S.obj[k];
+    const bool out_a = (ra > o.shell_hi) | (fabs(ra) + S.far_a < o.shell_lo);
+    const bool out_b = (rb > o.shell_hi) | (fabs(rb) + S.far_a < o.shell_lo);
+    ok = ok & ((o.kind == GRT_OBJ_DISC) ? ((north | south) & ratio) : (out_a & out_b));
+  }
+  bool fin = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) fin = fin & (bool)isfinite(yn[k]);
+  const double ar = fabs(rb), hi = ar + S.far_a;
+  return ok & fin & (rb > S.horizon_r) & (hi * hi < S.cel_lo2) & (i_next != S.max_steps - 1);
+}
+
 // The step-size controller of rkf45 (runge_kutta.rs:148-178) after one attempt with
 // error norm `err` at step h_cur.  Accepted: h_next is the next step's h.  Rejected:
 // h_cur is the retry's step (STEP_RETRY), or the 100th retry failed (STEP_FAILED,
@@ -1575,6 +1608,23 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
                               ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
                               : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
     n_att++;
+#if GRT_QUICK_STEP
+    if constexpr (G == GRT_GEOM_SCHWARZSCHILD && !VOL) {
+      // every lane of the wave on the commonest accepted step (quick_step_ok): the
+      // general path's updates in one straight-line block
+      if (__ballot(!quick_step_ok<G>(S, err_sq, y, yn, i + 1)) == 0) {
+        h = rclamp(h_cur * H_GROWTH, H_MIN, H_MAX);
+        i++;
+        n_acc++;
+        c_valid = false;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = yn[k];
+        retries = 0;
+        h_cur = rclamp(h, H_MIN, H_MAX);
+        continue;
+      }
+    }
+#endif
     double h_next;
     const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
     if (ctl != STEP_ACCEPTED) {
