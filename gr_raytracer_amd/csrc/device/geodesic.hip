@@ -1601,30 +1601,34 @@ __global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
 
     // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
     double yn[8];
+    double err_sq;
     // Kerr-Schild: the RHS dwarfs the saved products, and a second copy of its attempt
     // (+80 KB of code) is not worth them
     constexpr bool UNIT_H_COPY = GRT_UNIT_H && G != GRT_GEOM_KERR;
-    const double err_sq = (UNIT_H_COPY && __ballot(active && h_cur != 1.0) == 0)
-                              ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
-                              : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
-    n_att++;
-#if GRT_QUICK_STEP
-    if constexpr (G == GRT_GEOM_SCHWARZSCHILD && !VOL) {
-      // every lane of the wave on the commonest accepted step (quick_step_ok): the
-      // general path's updates in one straight-line block
-      if (__ballot(!quick_step_ok<G>(S, err_sq, y, yn, i + 1)) == 0) {
-        h = rclamp(h_cur * H_GROWTH, H_MIN, H_MAX);
-        i++;
-        n_acc++;
-        c_valid = false;
+    constexpr bool QUICK = GRT_QUICK_STEP && G == GRT_GEOM_SCHWARZSCHILD && !VOL;
+    while (true) {
+      err_sq = (UNIT_H_COPY && __ballot(active && h_cur != 1.0) == 0)
+                   ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
+                   : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
+      n_att++;
+      if constexpr (QUICK) {
+        // every lane of the wave on the commonest accepted step (quick_step_ok): the
+        // general path's updates in one straight-line block, then straight on to the next
+        // attempt (no ray ended, so no lane needs a refill)
+        if (__ballot(!quick_step_ok<G>(S, err_sq, y, yn, i + 1)) == 0) {
+          h = rclamp(h_cur * H_GROWTH, H_MIN, H_MAX);
+          i++;
+          n_acc++;
+          c_valid = false;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) y[k] = yn[k];
-        retries = 0;
-        h_cur = rclamp(h, H_MIN, H_MAX);
-        continue;
+          for (int k = 0; k < 8; ++k) y[k] = yn[k];
+          retries = 0;
+          h_cur = rclamp(h, H_MIN, H_MAX);
+          continue;
+        }
       }
+      break;
     }
-#endif
     double h_next;
     const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
     if (ctl != STEP_ACCEPTED) {
