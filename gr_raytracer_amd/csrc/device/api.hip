@@ -57,7 +57,6 @@ struct DeviceCopy {
   unsigned long long* d_march = nullptr;    // [0] jobs, [1] job cursor, [2] samples, [3] jobs (cumulative)
   bool vol = false;                         // the scene has VolumetricDiscs
   int cus = 0;
-  int blocks = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // calls on one device are serialised
   // integrate -> shade hand-off buffers, grown on demand (bytes per ray: ~1.1 KB)
@@ -355,8 +354,6 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   int occ = 0;
   void (*kfn)() = nullptr;
   (void)kfn;
-  int bpc = g_blocks_per_cu > 0 ? g_blocks_per_cu : 2 * GRT_INTEGRATE_WAVES;
-  dc.blocks = dc.cus * bpc;
   HIP_TRY(hipEventCreate(&dc.ev0));
   HIP_TRY(hipEventCreate(&dc.ev1));
   (void)occ;
@@ -479,7 +476,8 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
   if (dc.vol) HIP_TRY(hipMemsetAsync(dc.d_march, 0, 2 * sizeof(unsigned long long), stream));  // jobs, cursor
   int threads = g_threads;
-  int blocks = g_blocks_per_cu > 0 ? dc.cus * g_blocks_per_cu : dc.blocks;
+  int blocks = g_blocks_per_cu > 0 ? dc.cus * g_blocks_per_cu
+                                   : dc.cus * 2 * grt::integrate_waves(s->desc.geometry, dc.vol);
   // never launch more lanes than there is work for
   uint64_t max_blocks = (wl.n_items + threads - 1) / threads;
   if ((uint64_t)blocks > max_blocks) blocks = (int)std::max<uint64_t>(1, max_blocks);

@@ -150,8 +150,21 @@ inline uint32_t shard_frame_row(uint32_t band_rows, uint32_t shard, uint32_t n_s
 }
 
 #ifndef GRT_INTEGRATE_WAVES
-#define GRT_INTEGRATE_WAVES 2  // min waves per SIMD requested for the integrate kernel
+#define GRT_INTEGRATE_WAVES 2  // waves per SIMD of the Kerr-Schild and volumetric integrate kernels
 #endif
+#ifndef GRT_INTEGRATE_WAVES_LIGHT
+#define GRT_INTEGRATE_WAVES_LIGHT 3  // the other integrate kernels (<= 168 VGPRs)
+#endif
+// Waves per SIMD of integrate_kernel<geometry, vol> (its __launch_bounds__; the launch
+// puts twice that many blocks of 256 threads on each CU).  Kerr-Schild's RHS needs ~250
+// registers, the volumetric window records more; the Schwarzschild, KerrBL and flat
+// kernels fit 168 (measured: C2 -2%, C3 -10% at 3 waves).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr int integrate_waves(int geometry, bool vol) {
+  return (geometry == 2 /* GRT_GEOM_KERR */ || vol) ? GRT_INTEGRATE_WAVES : GRT_INTEGRATE_WAVES_LIGHT;
+}
 #ifndef GRT_TAIL_WAVES
 #define GRT_TAIL_WAVES 1  // waves per SIMD of the tail kernel: a lone wave owns its SIMD's issue slots
 #endif

@@ -59,27 +59,42 @@ namespace grt {
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
 
+// The OCML fallbacks below run outside glibc's fast paths only (never for the angles and
+// controller ratios of a render): out of line, so their code stays out of the hot loops.
+#ifndef GRT_SLOW_NOINLINE
+#define GRT_SLOW_NOINLINE 1
+#endif
+#if GRT_SLOW_NOINLINE
+#define GRT_SLOW __device__ __attribute__((noinline))
+#else
+#define GRT_SLOW GDEV
+#endif
+GRT_SLOW double ocml_pow(double x, double y) { return pow(x, y); }
+GRT_SLOW void ocml_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+GRT_SLOW double ocml_sin(double x) { return sin(x); }
+GRT_SLOW double ocml_cos(double x) { return cos(x); }
+
 // f64::powf == glibc pow: bit-exact on glibc's fast path, OCML outside it.
 GDEV double rpow(double x, double y) {
   double r;
   if (glibc::pow_fast(x, y, &r)) return r;
-  return pow(x, y);
+  return ocml_pow(x, y);
 }
 // f64::sin / f64::cos of one operand in one reference function: the compiler fuses
 // them into glibc's sincos (glibc_math.h); a lone sin() stays glibc's sin.  Both are
 // bit-exact for |x| < 105414350; OCML beyond (never reached by angles here).
 GDEV void rsincos(double x, double* s, double* c) {
-  if (!glibc::sincos_fast(x, s, c)) sincos(x, s, c);
+  if (!glibc::sincos_fast(x, s, c)) ocml_sincos(x, s, c);
 }
 GDEV double rsin(double x) {
   double r;
   if (glibc::sin_fast(x, &r)) return r;
-  return sin(x);
+  return ocml_sin(x);
 }
 GDEV double rcos(double x) {
   double r;
   if (glibc::cos_fast(x, &r)) return r;
-  return cos(x);
+  return ocml_cos(x);
 }
 
 // x1 / y and x2 / y with one reciprocal refinement.  This is the compiler's own IEEE f64
@@ -1429,7 +1444,7 @@ GDEV unsigned long long load_agent(const unsigned long long* p) {
 // Kerr-Schild with tl.cap != 0: once the tile queue is drained and at most tl.threshold
 // rays are live, each wave hands its rays to tail_kernel (tail_save) and exits.
 template <int G, bool VOL>
-__global__ void __launch_bounds__(256, GRT_INTEGRATE_WAVES) integrate_kernel(
+__global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel(
     const DevScene* __restrict__ Sp, WorkList wl, Workspace ws, unsigned long long* __restrict__ counter,
     unsigned long long* __restrict__ stats, TailList tl) {
   const DevScene& S = *Sp;
