@@ -542,7 +542,10 @@ int grt_tonemap_async(int device, void* stream, const double* d_xyza, uint64_t n
 int grt_xyz_to_srgb8_device(int device, const double* xyza, size_t n, int32_t tone_mapping,
                             double exposure, uint8_t* rgb_out);
 
-/* Kernel launch geometry knobs (persistent grid). 0 = library default. */
+/* Kernel launch geometry knobs (persistent grid). 0 = library default: 256 threads per
+ * block, 2w blocks per CU for an integrate kernel that keeps w waves per SIMD resident
+ * (w = 3 for Schwarzschild, KerrBL and the flat charts; 2 for Kerr-Schild and scenes with
+ * a VolumetricDisc).  Scheduling only: results are identical for every shape. */
 int grt_set_launch_config(int blocks_per_cu, int threads_per_block);
 /* Tile queue order of rectangle / shard traces: 0 = row-major 8x8 tiles; 1 = a probe
  * pass (one capped ray per tile) then the tiles with the longest predicted rays first;
