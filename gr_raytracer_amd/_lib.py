@@ -12,7 +12,7 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("GRT_LIB", str(PKG_DIR / "lib" / "libgrt.so")))
 
-GRT_ABI_VERSION = 2
+GRT_ABI_VERSION = 3
 GRT_MAX_OBJECTS = 8
 GRT_MAX_HITS = 16
 
@@ -105,7 +105,8 @@ class Offsets(C.Structure):
 
 
 class AuxOut(C.Structure):
-    _fields_ = [("xyza64", _pd), ("steps", C.POINTER(C.c_uint32)), ("stop_reason", C.POINTER(C.c_uint8))]
+    _fields_ = [("xyza64", _pd), ("steps", C.POINTER(C.c_uint32)), ("stop_reason", C.POINTER(C.c_uint8)),
+                ("hits", C.POINTER(C.c_uint32))]
 
 
 class RowShard(C.Structure):
@@ -114,7 +115,8 @@ class RowShard(C.Structure):
 
 class SubsampleFailures(C.Structure):
     _fields_ = [("capacity", C.c_uint64), ("pixel", C.POINTER(C.c_uint32)), ("sample", C.POINTER(C.c_uint32)),
-                ("status", C.POINTER(C.c_uint8)), ("count", C.c_uint64)]
+                ("status", C.POINTER(C.c_uint8)), ("count", C.c_uint64), ("stop", C.POINTER(C.c_uint8)),
+                ("steps", C.POINTER(C.c_uint32))]
 
 
 class Health(C.Structure):
@@ -201,6 +203,8 @@ def lib() -> C.CDLL:
         "grt_render_shard": (C.c_int, [vp, C.c_int, C.POINTER(RowShard), C.POINTER(C.c_float), C.POINTER(C.c_uint8),
                                        C.POINTER(C.c_uint8), C.POINTER(AuxOut), C.POINTER(Stats)]),
         "grt_render_shard_async": (C.c_int, [vp, C.c_int, vp, C.POINTER(RowShard), vp, vp, vp, vp, vp, vp, vp]),
+        "grt_hit_pool_reserve": (C.c_int, [vp, C.c_int, u64, C.POINTER(C.c_uint64)]),
+        "grt_set_hit_pool_min": (C.c_int, [u64]),
         "grt_adaptive_min_luminance": (_d, [_pd, u64, C.POINTER(AdaptiveConfig)]),
         "grt_adaptive_min_luminance_device": (C.c_int, [C.c_int, vp, vp, u32, u64, C.POINTER(AdaptiveConfig),
                                                         C.POINTER(_d)]),
@@ -211,7 +215,8 @@ def lib() -> C.CDLL:
         "grt_adaptive_floor_device": (C.c_int, [vp, C.c_int, vp, vp, u32, u64, vp]),
         "grt_render_section_ex": (C.c_int, [vp, C.c_int, u32, u32, u32, u32, C.POINTER(AdaptiveConfig), _pd, _pd,
                                             C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(Stats),
-                                            C.POINTER(C.c_uint8), C.POINTER(SubsampleFailures)]),
+                                            C.POINTER(C.c_uint8), C.POINTER(SubsampleFailures),
+                                            C.POINTER(C.c_uint8), C.POINTER(C.c_uint32)]),
         "grt_write_png_rgb": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), u32, u32]),
         "grt_write_hdr_xyz": (C.c_int, [C.c_char_p, _pd, u32, u32]),
         "grt_linear_max_async": (C.c_int, [C.c_int, vp, vp, u64, _d, vp]),
@@ -245,7 +250,7 @@ EXPORTED_SYMBOLS = [
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
     "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_perlin_permutation", "grt_volumetric_frame", "grt_xyz_to_srgb8", "grt_xyz_to_srgb", "grt_blackbody_spectrum", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
     "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config", "grt_set_schedule", "grt_set_tail", "grt_tail_handoffs", "grt_health_pixels", "grt_tail_report",
-    "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async",
+    "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async", "grt_hit_pool_reserve", "grt_set_hit_pool_min",
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",
     "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_adaptive_min_luminance_device", "grt_supersample_shard",
     "grt_supersample_shard_device", "grt_adaptive_floor_device", "grt_render_section_ex",

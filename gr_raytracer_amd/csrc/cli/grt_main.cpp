@@ -117,6 +117,19 @@ static bool split_csv(const std::string& s, std::vector<double>& out) {
   return true;
 }
 
+// scene.rs:178-183, :196-202: color_of_ray's lines for an error-free ray that ended on NaN
+// coordinates or without a terminal event.  The Ray's Debug form is cut to its pixel
+// (row, col); steps.len() = accepted steps + the initial step.
+static void log_ray_event(unsigned row, unsigned col, int stop, uint32_t accepted) {
+  const unsigned long long len = (unsigned long long)accepted + 1;
+  if (stop == GRT_STOP_NAN)
+    std::fprintf(stderr, "[grt] ERROR Ray hit NaN coordinates: Ray { row: %u, col: %u, .. } with %llu steps.\n", row,
+                 col, len);
+  else if (stop == GRT_STOP_NONE)
+    std::fprintf(stderr, "[grt] ERROR Ray did not hit anything: Ray { row: %u, col: %u, .. } at Some(Step { .. }) "
+                 "with %llu steps.\n", row, col, len);
+}
+
 static const char* stop_name(int s) {  // integrator.rs StopReason, as logged by the reference
   switch (s) {
     case GRT_STOP_HORIZON: return "Some(HorizonReached)";
@@ -376,26 +389,51 @@ int main(int argc, char** argv) {
   // failed supersample sub-rays (raytracer.rs:357-362), up to 1M logged
   const uint64_t fail_cap = 1u << 20;
   std::vector<uint32_t> fail_pix(fail_cap), fail_sample(fail_cap);
-  std::vector<uint8_t> fail_status(fail_cap);
-  grt_subsample_failures fails{fail_cap, fail_pix.data(), fail_sample.data(), fail_status.data(), 0};
+  std::vector<uint8_t> fail_status(fail_cap), fail_stop(fail_cap);
+  std::vector<uint32_t> fail_steps(fail_cap);
+  grt_subsample_failures fails{fail_cap, fail_pix.data(), fail_sample.data(), fail_status.data(), 0,
+                               fail_stop.data(), fail_steps.data()};
+  std::vector<uint8_t> stop((size_t)w * h);
+  std::vector<uint32_t> steps((size_t)w * h);
+  const bool supersampled = ac.enabled || maskp;
+  if (supersampled)  // raytracer.rs:264-267
+    std::fprintf(stderr, "[grt] INFO Rendering section from (%u, %u) to (%u, %u) with supersampling\n", r0, c0, r1,
+                 c1);
   if (grt_render_section_ex(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st,
-                            status.data(), &fails)) {
+                            status.data(), &fails, stop.data(), steps.data())) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
-  // raytracer.rs:232-239: every pixel whose color_of_ray failed is logged (Debug form of
-  // the RaytracerError) and keeps the default colour
-  for (size_t i = 0; i < status.size(); ++i)
+  // The 1-spp pass, in pixel order (the reference logs from its parallel loop):
+  //  * raytracer.rs:232-239: a pixel whose color_of_ray failed (Debug form of the
+  //    RaytracerError); it keeps the default colour;
+  //  * scene.rs:178-183 / :196-202: an error-free ray that ended on NaN coordinates or
+  //    without a terminal event (steps.len() counts the initial step too).
+  for (size_t i = 0; i < status.size(); ++i) {
+    const unsigned col = (unsigned)(c0 + i % w), row = (unsigned)(r0 + i / w);
     if (status[i] & 0x7f)
-      std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n",
-                   (unsigned)(c0 + i % w), (unsigned)(r0 + i / w), error_debug_name(status[i] & 0x7f));
-  // :357-362: the same message for each failed sub-sample ray of a supersampled pixel
-  for (uint64_t k = 0; k < std::min<uint64_t>(fails.count, fail_cap); ++k)
-    std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n",
-                 (unsigned)(c0 + fail_pix[k] % w), (unsigned)(r0 + fail_pix[k] / w), error_debug_name(fail_status[k]));
-  if (fails.count > fail_cap)
-    std::fprintf(stderr, "[grt] ERROR %llu more failed sub-sample rays not listed\n",
-                 (unsigned long long)(fails.count - fail_cap));
+      std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n", col, row,
+                   error_debug_name(status[i] & 0x7f));
+    else
+      log_ray_event(row, col, stop[i], steps[i]);
+  }
+  if (supersampled && !maskp) {  // supersample (raytracer.rs:325), then its sub-rays' lines
+    std::fprintf(stderr, "[grt] INFO Supersampling %llu pixels\n", (unsigned long long)nsel);
+    // :357-362: the same error line for each failed sub-sample ray of a supersampled pixel
+    for (uint64_t k = 0; k < std::min<uint64_t>(fails.count, fail_cap); ++k) {
+      const unsigned col = (unsigned)(c0 + fail_pix[k] % w), row = (unsigned)(r0 + fail_pix[k] / w);
+      if (fail_status[k])
+        std::fprintf(stderr, "[grt] ERROR Unable to compute color for ray at pixel (%u, %u): %s\n", col, row,
+                     error_debug_name(fail_status[k]));
+      else
+        log_ray_event(row, col, fail_stop[k], fail_steps[k]);
+    }
+    if (fails.count > fail_cap)
+      std::fprintf(stderr, "[grt] ERROR %llu more failed or unterminated sub-sample rays not listed\n",
+                   (unsigned long long)(fails.count - fail_cap));
+  }
+  if (supersampled)  // raytracer.rs:313-316
+    std::fprintf(stderr, "[grt] INFO Finished rendering section from (%u, %u) to (%u, %u)\n", r0, c0, r1, c1);
   std::fprintf(stderr, "[grt] %llu rays, %llu accepted steps, %llu attempts, %llu supersampled pixels, kernel %.1f ms "
                "(%.3e steps/s)\n",
                (unsigned long long)st.rays, (unsigned long long)st.accepted_steps, (unsigned long long)st.attempts,

@@ -117,13 +117,12 @@ __global__ void offsets_kernel(const uint32_t* __restrict__ sel, uint64_t n_sel,
 
 // sel_out: output index per selected pixel; sel_px: its pixel index in the traced rect
 // (for the failure records).  A failed sub-sample (supersample's Err arm, :357-362) is
-// appended to fail_key (pixel * spa^2 + stratum) / fail_status when fail_cap allows;
-// fail_count counts them all.
+// appended to f.key (pixel * spa^2 + stratum) / f.status when f.cap allows; f.count
+// counts them all (and the NaN / no-terminal-event sub-rays when f.stop is set).
 __global__ void average_kernel(const uint32_t* __restrict__ sel_out, const uint32_t* __restrict__ sel_px,
                                uint64_t n_sel, const unsigned long long* d_count, uint64_t base, uint32_t spa,
                                const double* __restrict__ samples, const uint8_t* __restrict__ status,
-                               double* __restrict__ out, unsigned long long* fail_count, uint64_t* fail_key,
-                               uint8_t* fail_status, uint64_t fail_cap) {
+                               double* __restrict__ out, SubsampleFailures f) {
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_sel || (d_count && base + j >= *d_count)) return;
   uint64_t per = (uint64_t)spa * spa;
@@ -132,16 +131,22 @@ __global__ void average_kernel(const uint32_t* __restrict__ sel_out, const uint3
   for (uint64_t s = 0; s < per; ++s) {
     uint64_t k = j * per + s;
     const int st = status[k] & 0x7f;
-    if (st != GRT_OK) {
-      if (fail_count) {
-        const unsigned long long slot = atomicAdd(fail_count, 1ull);
-        if (slot < fail_cap) {
-          fail_key[slot] = (uint64_t)sel_px[j] * per + s;
-          fail_status[slot] = (uint8_t)st;
+    // scene.rs:178-183, :196-202: an error-free ray that hit NaN coordinates or no
+    // terminal event is logged by color_of_ray (the caller asked for those: f.stop)
+    const int stop = f.ray_stop ? f.ray_stop[k] : GRT_STOP_CELESTIAL;
+    const bool event = f.stop && st == GRT_OK && (stop == GRT_STOP_NAN || stop == GRT_STOP_NONE);
+    if ((st != GRT_OK || event) && f.count) {
+      const unsigned long long slot = atomicAdd(f.count, 1ull);
+      if (slot < f.cap) {
+        f.key[slot] = (uint64_t)sel_px[j] * per + s;
+        f.status[slot] = (uint8_t)st;
+        if (f.stop) {
+          f.stop[slot] = (uint8_t)stop;
+          f.steps[slot] = f.ray_steps ? f.ray_steps[k] : 0u;
         }
       }
-      continue;
     }
+    if (st != GRT_OK) continue;
     const double* c = samples + 4 * k;
     x = x + c[0];
     y = y + c[1];
@@ -305,7 +310,7 @@ hipError_t launch_average(const uint32_t* d_sel_out, const uint32_t* d_sel_px, u
                           const uint8_t* d_status, double* d_out, const SubsampleFailures& f, hipStream_t stream) {
   if (n_sel == 0) return hipSuccess;
   hipLaunchKernelGGL(average_kernel, dim3(nblocks(n_sel, 256)), dim3(256), 0, stream, d_sel_out, d_sel_px, n_sel,
-                     d_count, base, spa, d_samples, d_status, d_out, f.count, f.key, f.status, f.cap);
+                     d_count, base, spa, d_samples, d_status, d_out, f);
   return hipGetLastError();
 }
 hipError_t launch_paint(const uint32_t* d_sel, uint64_t n_sel, const unsigned long long* d_count, const double* mask,

@@ -52,7 +52,7 @@ struct DeviceCopy {
   bool ready = false;
   grt::DevScene* d_scene = nullptr;
   std::vector<void*> allocations;
-  unsigned long long* d_counter = nullptr;  // [0] work counter
+  unsigned long long* d_counter = nullptr;  // [0] work counter, [5..6] hit pool (HitPool::count)
   unsigned long long* d_stats = nullptr;    // [0..3] accepted, attempts, rays, overflows
   unsigned long long* d_march = nullptr;    // [0] jobs, [1] job cursor, [2] samples, [3] jobs (cumulative)
   bool vol = false;                         // the scene has VolumetricDiscs
@@ -74,23 +74,87 @@ struct DeviceCopy {
   unsigned long long* d_tail_ctl = nullptr;
   uint64_t tail_cap = 0;
   unsigned long long* tail_mem = nullptr;
+  // hit pool: window candidates past a ray's GRT_WS_SLOTS workspace slots, grow-only
+  uint64_t pool_cap = 0;
+  bool pool_vol = false;
+  void* pool_mem = nullptr;
+  uint64_t ws_jobs_pool = 0;  // pool capacity the workspace's raymarch job list was sized for
+  uint32_t *ws_head = nullptr, *ws_last = nullptr;  // per-ray list ends, carved from the workspace
+  grt::HitPool* d_pool = nullptr;  // the descriptor the kernels read (device memory)
+  grt::HitPool pool_desc{};        // what *d_pool holds
 };
+
+constexpr uint64_t POOL_MIN = 1ull << 20;            // records
+constexpr uint64_t POOL_MAX = (1ull << 31) - 1;      // job and list encodings hold 31 bits
+uint64_t g_pool_min = POOL_MIN;                      // grt_set_hit_pool_min (tests force a full pool)
+uint64_t pool_record_bytes(bool vol) { return 4 + 1 + 4 * 8 + 3 * 8 + 4 + 4 * 8 + 4 + (vol ? 3 * 8 + 4 * 8 : 0); }
+
+// Grow the hit pool to at least `want` records (never shrinks).
+int ensure_pool(DeviceCopy& dc, uint64_t want) {
+  want = std::min(std::max(want, g_pool_min), POOL_MAX);
+  if (want <= dc.pool_cap && dc.pool_mem && (!dc.vol || dc.pool_vol)) return 0;
+  want = std::max(want, dc.pool_cap);
+  if (dc.pool_mem) {
+    (void)hipDeviceSynchronize();  // earlier async launches may still use the old pool
+    (void)hipFree(dc.pool_mem);
+  }
+  dc.pool_mem = nullptr;
+  dc.pool_cap = 0;
+  if (hipMalloc(&dc.pool_mem, want * pool_record_bytes(dc.vol) + 16 * 256) != hipSuccess) {
+    (void)hipGetLastError();
+    dc.pool_mem = nullptr;
+    return fail(-ENOMEM, "cannot allocate the hit pool");
+  }
+  dc.pool_cap = want;
+  dc.pool_vol = dc.vol;
+  return 0;
+}
+
+grt::HitPool pool_view(const DeviceCopy& dc) {
+  grt::HitPool hp;
+  std::memset(&hp, 0, sizeof(hp));
+  hp.head = dc.ws_head;
+  hp.last = dc.ws_last;
+  const uint64_t m = dc.pool_cap;
+  char* p = (char*)dc.pool_mem;
+  auto take = [&](uint64_t bytes) {
+    char* r = p;
+    p += (bytes + 255) & ~255ull;
+    return (void*)r;
+  };
+  hp.cap = m;
+  hp.count = dc.d_counter + 5;
+  hp.p = (double*)take(4 * 8 * m);
+  hp.pt = (double*)take(3 * 8 * m);
+  hp.hcol = (double*)take(4 * 8 * m);
+  hp.win = (uint32_t*)take(4 * m);
+  hp.next = (uint32_t*)take(4 * m);
+  hp.hprev = (uint32_t*)take(4 * m);
+  hp.obj = (uint8_t*)take(m);
+  if (dc.pool_vol) {
+    hp.dir = (double*)take(3 * 8 * m);
+    hp.vcol = (double*)take(4 * 8 * m);
+  }
+  return hp;
+}
 
 // Carve a Workspace for n rays out of the device's grow-only arena.
 int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
-  const uint64_t M = GRT_MAX_HITS;
+  const uint64_t M = GRT_WS_SLOTS;
   const bool vol = dc.vol;
   // volumetric scenes: rc grows to 6 doubles; chord directions, raymarched colours, jobs
-  const uint64_t per_ray = 8 * 8 + (vol ? 6 : 4) * 8 + 1 + 1 + 1 + 4 + M * (4 + 1 + 4 * 8 + 3 * 8) +
+  const uint64_t per_ray = 8 * 8 + (vol ? 6 : 4) * 8 + 1 + 1 + 3 * 4 + 4 + M * (4 + 1 + 4 * 8 + 3 * 8) +
                            (vol ? M * (3 * 8 + 4 * 8 + 8) : 0);
-  if (n > dc.ws_cap || (vol && !dc.ws_vol)) {
+  // volumetric scenes: the raymarch job list also holds one job per pool record
+  const uint64_t jobs_extra = vol ? dc.pool_cap : 0;
+  if (n > dc.ws_cap || (vol && !dc.ws_vol) || jobs_extra > dc.ws_jobs_pool) {
     if (dc.ws_mem) {
       (void)hipDeviceSynchronize();  // earlier async launches may still use the old arena
       (void)hipFree(dc.ws_mem);
     }
     dc.ws_mem = nullptr;
     uint64_t cap = std::max<uint64_t>(n, 1 << 16);
-    if (hipMalloc(&dc.ws_mem, cap * per_ray + 32 * 256) != hipSuccess) {  // + per-array alignment
+    if (hipMalloc(&dc.ws_mem, cap * per_ray + jobs_extra * 8 + 32 * 256) != hipSuccess) {  // + per-array alignment
       (void)hipGetLastError();
       dc.ws_mem = nullptr;
       dc.ws_cap = 0;
@@ -98,6 +162,7 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
     }
     dc.ws_cap = cap;
     dc.ws_vol = vol;
+    dc.ws_jobs_pool = jobs_extra;
   }
   uint64_t cap = dc.ws_cap;
   char* p = (char*)dc.ws_mem;
@@ -115,7 +180,9 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   ws->rec_win = (uint32_t*)take(M * 4 * cap);
   ws->stop = (uint8_t*)take(cap);
   ws->status = (uint8_t*)take(cap);
-  ws->nrec = (uint8_t*)take(cap);
+  ws->nrec = (uint32_t*)take(4 * cap);
+  dc.ws_head = (uint32_t*)take(4 * cap);
+  dc.ws_last = (uint32_t*)take(4 * cap);
   ws->rec_obj = (uint8_t*)take(M * cap);
   ws->rec_dir = ws->vcol = nullptr;
   ws->jobs = nullptr;
@@ -124,7 +191,7 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   if (vol) {
     ws->rec_dir = (double*)take(3 * M * 8 * cap);
     ws->vcol = (double*)take(4 * M * 8 * cap);
-    ws->jobs = (uint64_t*)take(M * 8 * cap);
+    ws->jobs = (uint64_t*)take(M * 8 * cap + 8 * dc.ws_jobs_pool);
   }
   // the kernels index with the launch's n, which must not exceed the carved capacity
   if (n > cap) return fail(-ENOMEM, "workspace too small");
@@ -348,6 +415,10 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   dc.allocations.push_back(p);
   HIP_TRY(hipMemset(p, 0, 8 * sizeof(unsigned long long)));
   dc.d_tail_ctl = (unsigned long long*)p;
+  HIP_TRY(hipMalloc(&p, sizeof(grt::HitPool)));
+  dc.allocations.push_back(p);
+  HIP_TRY(hipMemset(p, 0, sizeof(grt::HitPool)));
+  dc.d_pool = (grt::HitPool*)p;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   dc.cus = prop.multiProcessorCount;
@@ -483,9 +554,21 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   if ((uint64_t)blocks > max_blocks) blocks = (int)std::max<uint64_t>(1, max_blocks);
   uint64_t n_out = wl.pixel_index ? wl.n_items : (uint64_t)wl.rows * wl.cols;
   grt::Workspace ws;
-  int rc = ensure_workspace(dc, n_out, &ws);
+  int rc = ensure_pool(dc, n_out / 2);
+  if (rc) return rc;
+  rc = ensure_workspace(dc, n_out, &ws);
   if (rc) return rc;
   ws.n_live = wl.n_live;
+  {  // the pool descriptor changes only when the pool or the workspace arena moved
+    const grt::HitPool hp = pool_view(dc);
+    if (std::memcmp(&hp, &dc.pool_desc, sizeof(hp)) != 0) {
+      HIP_TRY(hipDeviceSynchronize());  // no kernel in flight reads the old one
+      HIP_TRY(hipMemcpy(dc.d_pool, &hp, sizeof(hp), hipMemcpyHostToDevice));
+      dc.pool_desc = hp;
+    }
+  }
+  ws.pool = dc.d_pool;
+  HIP_TRY(hipMemsetAsync(dc.pool_desc.count, 0, sizeof(unsigned long long), stream));
   grt::TailList tl;
   int tail_blocks = 0;
   rc = tail_list(s, dc, blocks * (uint64_t)threads, &tl, &tail_blocks);
@@ -645,6 +728,7 @@ int grt_scene_destroy(grt_scene* s) {
     if (dc->sched_mem) (void)hipFree(dc->sched_mem);
     if (dc->ad_mem) (void)hipFree(dc->ad_mem);
     if (dc->tail_mem) (void)hipFree(dc->tail_mem);
+    if (dc->pool_mem) (void)hipFree(dc->pool_mem);
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
     delete dc;
@@ -659,32 +743,50 @@ static int check_rect(const grt_scene* s, uint64_t row0, uint64_t col0, uint64_t
   return 0;
 }
 
+// Synchronous calls: after the work has finished, whether some trace needed more hit-pool
+// records than it had.  If so the pool is grown to that size (*again = true): the call
+// traces again, and the deterministic trace then keeps every candidate.
+static int pool_check(DeviceCopy& dc, bool* again) {
+  unsigned long long need = 0;
+  HIP_TRY(hipMemcpy(&need, dc.d_counter + 6, sizeof(need), hipMemcpyDeviceToHost));
+  *again = need > dc.pool_cap && dc.pool_cap < POOL_MAX;
+  if (*again) return ensure_pool(dc, need + need / 4);
+  return 0;
+}
+
 // Trace `wl` (n output slots) into device scratch, wait, copy to the host arrays.
 static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, uint64_t n, float* xyza_out,
                        uint8_t* class_out, uint8_t* status_out, const grt_aux_out* aux, grt_stats* stats) {
   int rc;
   DeviceCopy* dc = dc_;
-  DevBuf b_xyza, b_cls, b_status, b_x64, b_steps, b_stop;
+  DevBuf b_xyza, b_cls, b_status, b_x64, b_steps, b_stop, b_hits;
   if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n))) return rc;
   bool want64 = aux && aux->xyza64, want_steps = aux && aux->steps, want_stop = aux && aux->stop_reason;
+  bool want_hits = aux && aux->hits;
   if (want64 && (rc = b_x64.alloc(n * 32))) return rc;
   if (want_steps && (rc = b_steps.alloc(n * 4))) return rc;
   if (want_stop && (rc = b_stop.alloc(n))) return rc;
+  if (want_hits && (rc = b_hits.alloc(n * 4))) return rc;
   grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p,
-                 (uint32_t*)b_steps.p, (uint8_t*)b_stop.p};
+                 (uint32_t*)b_steps.p, (uint8_t*)b_stop.p, (uint32_t*)b_hits.p};
   hipStream_t st = nullptr;
-  HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
-  HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
-  HIP_TRY(hipEventRecord(dc->ev0, st));
-  if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
-  HIP_TRY(hipEventRecord(dc->ev1, st));
-  HIP_TRY(hipEventSynchronize(dc->ev1));
+  for (bool again = true; again;) {
+    HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(dc->d_counter + 6, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(dc->ev0, st));
+    if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
+    HIP_TRY(hipEventRecord(dc->ev1, st));
+    HIP_TRY(hipEventSynchronize(dc->ev1));
+    if ((rc = pool_check(*dc, &again))) return rc;
+  }
   HIP_TRY(hipMemcpy(xyza_out, b_xyza.p, n * 16, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
   if (want64) HIP_TRY(hipMemcpy(aux->xyza64, b_x64.p, n * 32, hipMemcpyDeviceToHost));
   if (want_steps) HIP_TRY(hipMemcpy(aux->steps, b_steps.p, n * 4, hipMemcpyDeviceToHost));
   if (want_stop) HIP_TRY(hipMemcpy(aux->stop_reason, b_stop.p, n, hipMemcpyDeviceToHost));
+  if (want_hits) HIP_TRY(hipMemcpy(aux->hits, b_hits.p, n * 4, hipMemcpyDeviceToHost));
   if (stats) {
     unsigned long long h[4];
     HIP_TRY(hipMemcpy(h, dc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
@@ -905,7 +1007,8 @@ struct SuperBufs {
   uint32_t* pix = nullptr;
   double *dx = nullptr, *dy = nullptr, *x64 = nullptr;
   float* xyza = nullptr;
-  uint8_t *cls = nullptr, *status = nullptr;
+  uint8_t *cls = nullptr, *status = nullptr, *stop = nullptr;
+  uint32_t* steps = nullptr;
   unsigned long long* live = nullptr;
   void carve(AdArena& A, uint64_t n_max, uint32_t spa) {
     per = spa * spa;
@@ -919,6 +1022,8 @@ struct SuperBufs {
     cls = (uint8_t*)A.take(cap);
     status = (uint8_t*)A.take(cap);
     x64 = (double*)A.take(cap * 32);
+    stop = (uint8_t*)A.take(cap);
+    steps = (uint32_t*)A.take(cap * 4);
     live = (unsigned long long*)A.take((uint64_t)n_chunks * 8);
   }
 };
@@ -931,7 +1036,10 @@ struct SuperBufs {
 static int enqueue_supersample(grt_scene* s, DeviceCopy& dc, hipStream_t st, const SuperBufs& B, uint32_t row0,
                         uint32_t col0, uint32_t rows, uint32_t cols, const uint32_t* sel_px, const uint32_t* sel_out,
                         const unsigned long long* d_count, uint32_t spa, double* d_out64, unsigned long long* d_stats,
-                        const grt::SubsampleFailures& fails) {
+                        const grt::SubsampleFailures& fails_in) {
+  grt::SubsampleFailures fails = fails_in;
+  fails.ray_stop = B.stop;
+  fails.ray_steps = B.steps;
   HIP_TRY(grt::launch_chunk_live(d_count, B.n_chunks, B.chunk_pix, B.per, B.live, st));
   for (uint32_t c = 0; c < B.n_chunks; ++c) {
     const uint64_t base = (uint64_t)c * B.chunk_pix;
@@ -948,7 +1056,7 @@ static int enqueue_supersample(grt_scene* s, DeviceCopy& dc, hipStream_t st, con
     wo.dx = B.dx;
     wo.dy = B.dy;
     wo.n_live = B.live + c;
-    grt::Outputs so{B.xyza, B.cls, B.status, B.x64, nullptr, nullptr};
+    grt::Outputs so{B.xyza, B.cls, B.status, B.x64, B.steps, B.stop};
     int rc = enqueue_trace(s, dc, wo, so, d_stats, st);
     if (rc) return rc;
     HIP_TRY(grt::launch_average(sel_out + base, sel_px + base, B.chunk_pix, d_count, base, spa, B.x64, B.status,
@@ -1011,9 +1119,14 @@ static int copy_failures(const grt::SubsampleFailures& f, uint64_t count, uint32
   const uint64_t m = std::min<uint64_t>(count, f.cap);
   if (m == 0) return 0;
   std::vector<uint64_t> key(m);
-  std::vector<uint8_t> st(m);
+  std::vector<uint8_t> st(m), sp(f.stop ? m : 0);
+  std::vector<uint32_t> ns(f.stop ? m : 0);
   HIP_TRY(hipMemcpy(key.data(), f.key, m * 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(st.data(), f.status, m, hipMemcpyDeviceToHost));
+  if (f.stop) {
+    HIP_TRY(hipMemcpy(sp.data(), f.stop, m, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ns.data(), f.steps, m * 4, hipMemcpyDeviceToHost));
+  }
   std::vector<uint64_t> order(m);
   for (uint64_t i = 0; i < m; ++i) order[i] = i;
   std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return key[a] < key[b]; });
@@ -1022,6 +1135,10 @@ static int copy_failures(const grt::SubsampleFailures& f, uint64_t count, uint32
     out->pixel[i] = (uint32_t)(key[order[i]] / per);
     if (out->sample) out->sample[i] = (uint32_t)(key[order[i]] % per);
     out->status[i] = st[order[i]];
+    if (f.stop) {
+      out->stop[i] = sp[order[i]];
+      if (out->steps) out->steps[i] = ns[order[i]];
+    }
   }
   return 0;
 }
@@ -1029,7 +1146,7 @@ static int copy_failures(const grt::SubsampleFailures& f, uint64_t count, uint32
 int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t from_col, uint32_t to_row,
                           uint32_t to_col, const grt_adaptive_config* cfg, const double* mask_xyza, double* xyza_out,
                           uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats, uint8_t* status_out,
-                          grt_subsample_failures* failures) {
+                          grt_subsample_failures* failures, uint8_t* stop_out, uint32_t* steps_out) {
   if (!s || !cfg || !xyza_out) return fail(-EINVAL, "null argument");
   if (to_row < from_row || to_col < from_col) return fail(-EINVAL, "empty section");
   if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
@@ -1055,7 +1172,10 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
   if (device_floor) HIP_TRY(grt::luminance_floor_device(nullptr, 4, n, floor_index(n), nullptr, &sort_bytes, nullptr, 0));
   if (supersampled) HIP_TRY(grt::compact_flags(nullptr, n, nullptr, nullptr, nullptr, &select_bytes, 0));
   const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
+  const bool want_events = fail_cap && failures->stop;
   grt::SubsampleFailures fails{nullptr, nullptr, nullptr, fail_cap};
+  uint8_t* b_stop = nullptr;
+  uint32_t* b_steps = nullptr;
   auto carve = [&](AdArena& A, float** xyza, uint8_t** cls, uint8_t** status, double** x64, uint8_t** flags,
                    uint32_t** sel, unsigned long long** cnt, double** floor, void** sort, void** select,
                    SuperBufs* B) {
@@ -1063,6 +1183,8 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
     *cls = (uint8_t*)A.take(n);
     *status = (uint8_t*)A.take(n);
     *x64 = (double*)A.take(n * 32);
+    if (stop_out) b_stop = (uint8_t*)A.take(n);
+    if (steps_out) b_steps = (uint32_t*)A.take(n * 4);
     if (!supersampled) return;
     *flags = (uint8_t*)A.take(n);
     *sel = (uint32_t*)A.take(n * 4);
@@ -1073,6 +1195,10 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
     if (!mask_xyza) B->carve(A, n, spa);
     fails.key = (uint64_t*)A.take(fail_cap * 8);
     fails.status = (uint8_t*)A.take(fail_cap);
+    if (want_events) {  // NaN / no-terminal-event sub-rays too (scene.rs:178-183, :196-202)
+      fails.stop = (uint8_t*)A.take(fail_cap);
+      fails.steps = (uint32_t*)A.take(fail_cap * 4);
+    }
   };
   float* b_xyza = nullptr;
   uint8_t *b_cls = nullptr, *b_status = nullptr, *b_flags = nullptr;
@@ -1089,12 +1215,14 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
     carve(A, &b_xyza, &b_cls, &b_status, &b_x64, &b_flags, &b_sel, &d_cnt, &d_floor, &b_sort, &b_select, &B);
   }
   hipStream_t st = nullptr;
+  for (bool again = true; again;) {
   HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
   HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc->d_counter + 6, 0, sizeof(unsigned long long), st));
   if (supersampled) HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, st));
   HIP_TRY(hipEventRecord(dc->ev0, st));
   grt::WorkList wl = rect_worklist(from_row, from_col, h, w);
-  grt::Outputs o{b_xyza, b_cls, b_status, b_x64, nullptr, nullptr};
+  grt::Outputs o{b_xyza, b_cls, b_status, b_x64, b_steps, b_stop};
   if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
   if (supersampled) {
     // resolve_minimum_luminance (raytracer.rs:118-129): the exact 99th percentile in
@@ -1123,9 +1251,13 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
   }
   HIP_TRY(hipEventRecord(dc->ev1, st));
   HIP_TRY(hipEventSynchronize(dc->ev1));
+  if ((rc = pool_check(*dc, &again))) return rc;
+  }
   HIP_TRY(hipMemcpy(xyza_out, b_x64, n * 32, hipMemcpyDeviceToHost));
   if (class_out) HIP_TRY(hipMemcpy(class_out, b_cls, n, hipMemcpyDeviceToHost));
   if (status_out) HIP_TRY(hipMemcpy(status_out, b_status, n, hipMemcpyDeviceToHost));
+  if (stop_out) HIP_TRY(hipMemcpy(stop_out, b_stop, n, hipMemcpyDeviceToHost));
+  if (steps_out) HIP_TRY(hipMemcpy(steps_out, b_steps, n * 4, hipMemcpyDeviceToHost));
   if (supersampled) {
     unsigned long long cnt[2] = {0, 0};
     HIP_TRY(hipMemcpy(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
@@ -1160,7 +1292,7 @@ int grt_render_section(grt_scene* s, int device, uint32_t from_row, uint32_t fro
                        double* xyza_out, uint8_t* class_out, uint64_t* n_supersampled, grt_stats* stats,
                        uint8_t* status_out) {
   return grt_render_section_ex(s, device, from_row, from_col, to_row, to_col, cfg, mask_xyza, xyza_out, class_out,
-                               n_supersampled, stats, status_out, nullptr);
+                               n_supersampled, stats, status_out, nullptr, nullptr, nullptr);
 }
 
 
@@ -1213,6 +1345,32 @@ int grt_render_shard(grt_scene* s, int device, const grt_row_shard* sh, float* x
   return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
 }
 
+int grt_set_hit_pool_min(uint64_t records) {
+  if (records == 0 || records > POOL_MAX) return fail(-EINVAL, "hit pool minimum must be in [1, 2^31)");
+  g_pool_min = records;
+  return 0;
+}
+
+int grt_hit_pool_reserve(grt_scene* s, int device, uint64_t records, uint64_t* capacity) {
+  if (!s) return fail(-EINVAL, "null argument");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  if (records == 0) {  // the largest need since the last reset, once the device is idle
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long need = 0;
+    HIP_TRY(hipMemcpy(&need, dc->d_counter + 6, sizeof(need), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(dc->d_counter + 6, 0, sizeof(need)));
+    records = need + need / 4;
+  }
+  if (records > POOL_MAX) return fail(-ENOMEM, "hit pool larger than 2^31 records");
+  if ((rc = ensure_pool(*dc, records))) return rc;
+  if (capacity) *capacity = dc->pool_cap;
+  return 0;
+}
+
 int grt_render_shard_async(grt_scene* s, int device, void* stream, const grt_row_shard* sh, float* d_xyza,
                            uint8_t* d_class, uint8_t* d_status, double* d_xyza64, uint32_t* d_steps,
                            uint8_t* d_stop, uint64_t* d_stats) {
@@ -1254,6 +1412,7 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
   if (n_local > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "shard larger than INT_MAX pixels");
   const uint32_t spa = cfg->samples_per_axis;
   const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
+  const bool want_events = fail_cap && failures->stop;
   size_t select_bytes = 0;
   HIP_TRY(grt::compact_flags(nullptr, n_local, nullptr, nullptr, nullptr, &select_bytes, 0));
   uint8_t* b_flags = nullptr;
@@ -1271,6 +1430,10 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
     if (!sampling_mask_xyza) B.carve(A, n_local, spa);
     fails.key = (uint64_t*)A.take(fail_cap * 8);
     fails.status = (uint8_t*)A.take(fail_cap);
+    if (want_events) {  // NaN / no-terminal-event sub-rays too (scene.rs:178-183, :196-202)
+      fails.stop = (uint8_t*)A.take(fail_cap);
+      fails.steps = (uint32_t*)A.take(fail_cap * 4);
+    }
   };
   {
     AdArena plan;

@@ -6,6 +6,13 @@
 #pragma once
 #include <stdint.h>
 
+// Window candidates a ray keeps in workspace slots before the hit pool (grt_api.h
+// GRT_MAX_HITS).  Overridable at build time: a build with very few slots sends nearly
+// every candidate through the pool, which the parity tests then cover.
+#ifndef GRT_WS_SLOTS
+#define GRT_WS_SLOTS GRT_MAX_HITS
+#endif
+
 namespace grt {
 
 struct DevTexture {
@@ -112,17 +119,47 @@ struct WorkList {
   const unsigned long long* n_live;
 };
 
+// Window candidates of a ray beyond its GRT_WS_SLOTS workspace slots (the reference keeps
+// every window's intersection, scene.rs:139-152).  The integrate / tail kernels append
+// one record per candidate (one atomic each; rays with more than GRT_WS_SLOTS candidates
+// are rare) and link a ray's records in window order through `next`; the shade kernel
+// walks that list after the workspace slots.  Structure of arrays with stride `cap`.
+// A trace that needs more than `cap` records loses the rest: the pixel gets
+// GRT_FLAG_HIT_OVERFLOW and the synchronous entry points grow the pool and trace again.
+// The descriptor lives in device memory (Workspace::pool): the kernels load its fields
+// only on the rare paths that use them, so the persistent integrate kernels carry one
+// pointer for it, not a dozen (their scalar registers are scarce).
+constexpr uint32_t HIT_NIL = 0xffffffffu;
+struct HitPool {
+  uint64_t cap;              // records (< 2^31)
+  unsigned long long* count; // [0] records requested by this trace (may exceed cap),
+                             // [1] the largest [0] of the traces since the host reset it
+  uint32_t* win;             // [cap] window (accepted-step) index
+  uint8_t* obj;              // [cap] object index
+  double* p;                 // [4][cap] lerped momentum
+  double* pt;                // [3][cap] hit point
+  uint32_t* next;            // [cap] the ray's next record
+  double* hcol;              // [4][cap] shade kernel: colour of a window-nearest hit
+  uint32_t* hprev;           // [cap] shade kernel: the ray's previous window-nearest pool record
+  double* dir;               // [3][cap] volumetric scenes: chord direction
+  double* vcol;              // [4][cap] volumetric scenes: raymarched colour
+  uint32_t* head;            // [n] per ray: pool record of candidate GRT_WS_SLOTS
+  uint32_t* last;            // [n] per ray: pool record of the last candidate appended,
+                             //     HIT_NIL once one was lost
+};
+
 // Hand-off from the integrate kernel to the shade kernel, structure-of-arrays with
 // n = number of output slots of the launch.  Per ray: final state y[8], the per-ray
 // constants (observer energy, KerrBL E / L_z / Q), stop reason, status, step count
-// and up to GRT_MAX_HITS window candidates (slot-major: slot k of ray i at k*n + i).
+// and its window candidates: the first GRT_WS_SLOTS in slots (slot-major: slot k of ray
+// i at k*n + i), the rest in the hit pool.
 struct Workspace {
   uint64_t n;
   double* y;          // [8][n]
   double* rc;         // [4][n], [6][n] with volumetric objects (+ p_t, p_phi)
   uint8_t* stop;      // [n]
   uint8_t* status;    // [n]
-  uint8_t* nrec;      // [n] candidates recorded (saturating at 255)
+  uint32_t* nrec;     // [n] candidates recorded
   uint32_t* steps;    // [n]
   uint32_t* rec_win;  // [MAX][n] window (accepted-step) index
   uint8_t* rec_obj;   // [MAX][n] object index
@@ -131,13 +168,16 @@ struct Workspace {
   // volumetric scenes only (NULL otherwise)
   double* rec_dir;    // [3][MAX][n] chord direction y_end - y_start (volumetric candidates)
   double* vcol;       // [4][MAX][n] raymarched colour of volumetric candidate slots
-  uint64_t* jobs;     // [MAX * n] raymarch jobs: (ray << 8) | candidate slot
+  uint64_t* jobs;     // [MAX * n + pool.cap] raymarch jobs: (ray << 8) | candidate slot, or
+                      // JOB_POOL | ray << 31 | pool record
   unsigned long long* march;  // [0] job count, [1] job cursor, [2] samples, [3] jobs (cumulative),
                               // [4] samples that evaluated the noise, [5] samples that emitted
   // rays present when the count is decided on the device: min(*n_live, n) (NULL = n);
   // n stays the SoA stride
   const unsigned long long* n_live;
+  const HitPool* pool;  // device memory
 };
+constexpr uint64_t JOB_POOL = 1ull << 63;
 
 // Local row -> frame row under cyclic row-band sharding: band k of shard s is frame
 // band k * n_shards + s (grt_api.h, grt_row_shard).
@@ -194,6 +234,7 @@ struct Outputs {
   double* xyza64;     // optional
   uint32_t* steps;    // optional
   uint8_t* stop;      // optional
+  uint32_t* hits;     // optional: windows with an intersection (scene.rs:148, before any error)
 };
 
 }  // namespace grt

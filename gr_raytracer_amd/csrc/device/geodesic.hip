@@ -1332,8 +1332,39 @@ GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, int stop
   for (int k = 0; k < 8; ++k) ws.y[k * n + idx] = y[k];
   ws.stop[idx] = (uint8_t)stop;
   ws.status[idx] = (uint8_t)status;
-  ws.nrec[idx] = nrec > 255u ? 255u : nrec;
+  ws.nrec[idx] = nrec;
   ws.steps[idx] = steps;
+}
+
+// Candidate nrec >= GRT_WS_SLOTS of ray idx: one record appended to the hit pool and
+// linked after the ray's previous one.  Once a record does not fit, the ray's list is
+// marked lost (ovf_last = HIT_NIL) and nothing more is linked; the count keeps growing so
+// that the host learns the size the trace needed.
+GDEV void hit_append(const Workspace& ws, uint64_t idx, uint32_t nrec, uint32_t win, uint32_t obj,
+                     const double* p, const double* pt, const double* dir) {
+  const HitPool& hp = *ws.pool;
+  const unsigned long long pos = atomicAdd(hp.count, 1ull);
+  const bool first = nrec == GRT_WS_SLOTS;
+  const uint32_t prev = first ? HIT_NIL : ws.pool->last[idx];
+  if (pos >= hp.cap || (!first && prev == HIT_NIL)) {
+    if (first) ws.pool->head[idx] = HIT_NIL;
+    ws.pool->last[idx] = HIT_NIL;
+    return;
+  }
+  const uint64_t m = hp.cap;
+  hp.win[pos] = win;
+  hp.obj[pos] = (uint8_t)obj;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) hp.p[q * m + pos] = p[q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) hp.pt[q * m + pos] = pt[q];
+  if (dir) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) hp.dir[q * m + pos] = dir[q];
+  }
+  if (first) ws.pool->head[idx] = (uint32_t)pos;
+  else hp.next[prev] = (uint32_t)pos;
+  ws.pool->last[idx] = (uint32_t)pos;
 }
 
 // The window (y -> yn) of accepted step i against every object in config order
@@ -1367,7 +1398,7 @@ GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc
       double distance = sqrt(dx * dx + dy * dy + dz * dz);
       if (!(distance < shortest)) continue;
       shortest = distance;
-      if (writer && nrec < GRT_MAX_HITS) {
+      if (writer && nrec < GRT_WS_SLOTS) {
         double pa[4], pb[4];
         momentum<G>(S, rc, y, pa);
         momentum<G>(S, rc, yn, pb);
@@ -1376,14 +1407,23 @@ GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc
         ws.rec_win[slot] = (uint32_t)i;
         ws.rec_obj[slot] = (uint8_t)k;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot] = sw * pa[q] + t * pb[q];
+        for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_WS_SLOTS * n + slot] = sw * pa[q] + t * pb[q];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot] = pt[q];
+        for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_WS_SLOTS * n + slot] = pt[q];
         if constexpr (VOL) {  // chord direction for the raymarch (volumetric_disc.rs:576, :589-594)
           ws.rec_dir[slot] = cn[0] - c[0];
-          ws.rec_dir[(uint64_t)GRT_MAX_HITS * n + slot] = cn[1] - c[1];
-          ws.rec_dir[(uint64_t)2 * GRT_MAX_HITS * n + slot] = cn[2] - c[2];
+          ws.rec_dir[(uint64_t)GRT_WS_SLOTS * n + slot] = cn[1] - c[1];
+          ws.rec_dir[(uint64_t)2 * GRT_WS_SLOTS * n + slot] = cn[2] - c[2];
         }
+      } else if (writer) {  // beyond the workspace slots: the hit pool
+        double pa[4], pb[4], ph[4];
+        momentum<G>(S, rc, y, pa);
+        momentum<G>(S, rc, yn, pb);
+        double sw = 1.0 - t;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ph[q] = sw * pa[q] + t * pb[q];
+        double dir[3] = {cn[0] - c[0], cn[1] - c[1], cn[2] - c[2]};
+        hit_append(ws, idx, nrec, (uint32_t)i, k, ph, pt, VOL ? dir : nullptr);
       }
       nrec++;
     }
@@ -2182,7 +2222,8 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
 }
 
 GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, int status, int stop,
-                    uint32_t steps) {
+                    uint32_t steps, uint32_t hits) {
+  if (out.hits) out.hits[idx] = hits;
   reinterpret_cast<float4*>(out.xyza)[idx] = make_float4((float)c.x, (float)c.y, (float)c.z, (float)c.a);
   out.cls[idx] = (uint8_t)cls;
   out.status[idx] = (uint8_t)status;
@@ -2197,30 +2238,83 @@ GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, in
   if (out.stop) out.stop[idx] = (uint8_t)stop;
 }
 
+// ---- a ray's candidates in window order: workspace slots 0..GRT_WS_SLOTS-1, then the
+// hit pool's list (HitPool).
+struct RecRef {
+  bool pool;
+  uint64_t s;  // workspace slot j * n + idx, or pool record
+};
+// Candidates a ray can replay in order: all of them, unless its pool list was lost
+// (the pool was full), in which case only the workspace slots (*lost = true).
+GDEV uint32_t rec_count(const Workspace& ws, uint64_t idx, bool* lost) {
+  const uint32_t nrec = ws.nrec[idx];
+  *lost = nrec > GRT_WS_SLOTS && ws.pool->last[idx] == HIT_NIL;
+  return *lost ? GRT_WS_SLOTS : nrec;
+}
+// Candidate j, for j = 0, 1, 2, ... in turn (*pos carries the position in the pool list).
+GDEV RecRef rec_at(const Workspace& ws, uint64_t idx, uint32_t j, uint32_t* pos) {
+  if (j < GRT_WS_SLOTS) return RecRef{false, (uint64_t)j * ws.n + idx};
+  *pos = (j == GRT_WS_SLOTS) ? ws.pool->head[idx] : ws.pool->next[*pos];
+  return RecRef{true, *pos};
+}
+GDEV uint32_t rec_win(const Workspace& ws, const RecRef& r) { return r.pool ? ws.pool->win[r.s] : ws.rec_win[r.s]; }
+// The window of candidate j + 1 (which exists), given candidate j.
+GDEV uint32_t rec_next_win(const Workspace& ws, uint64_t idx, uint32_t j, const RecRef& r) {
+  if (j + 1 < GRT_WS_SLOTS) return ws.rec_win[r.s + ws.n];
+  if (j + 1 == GRT_WS_SLOTS) return ws.pool->win[ws.pool->head[idx]];
+  return ws.pool->win[ws.pool->next[r.s]];
+}
+GDEV uint32_t rec_read(const Workspace& ws, const RecRef& r, double* p, double* pt) {
+  if (!r.pool) {
+    const uint64_t MN = (uint64_t)GRT_WS_SLOTS * ws.n;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[q * MN + r.s];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[q * MN + r.s];
+    return ws.rec_obj[r.s];
+  }
+  const uint64_t m = ws.pool->cap;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = ws.pool->p[q * m + r.s];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) pt[q] = ws.pool->pt[q * m + r.s];
+  return ws.pool->obj[r.s];
+}
+
 // Volumetric scenes, pass 1: the candidate slots whose raymarched colour the composite
 // needs -- the window-nearest VolumetricDisc hits of a ray whose window pass raises no
 // error (an error aborts the pixel, scene.rs:146, so its marches would be wasted).
+// Workspace slots come back as a mask; pool records get their jobs appended here.
 template <int G>
 GDEV uint32_t march_slots(const DevScene& S, const Workspace& ws, uint64_t idx) {
   const uint64_t n = ws.n;
   if (ws.status[idx] != GRT_OK) return 0u;
   RayConst rc{ws.rc[idx], ws.rc[n + idx], ws.rc[2 * n + idx], ws.rc[3 * n + idx]};
-  uint32_t nrec = ws.nrec[idx];
-  uint32_t nr = nrec < GRT_MAX_HITS ? nrec : GRT_MAX_HITS;
-  uint32_t mask = 0u;
+  bool lost;
+  const uint32_t nr = rec_count(ws, idx, &lost);
+  uint32_t mask = 0u, pool_jobs = 0u, pos = HIT_NIL;
   for (uint32_t j = 0; j < nr; ++j) {
-    const uint64_t slot = (uint64_t)j * n + idx;
-    uint32_t win = ws.rec_win[slot];
-    const DevObject& o = S.obj[ws.rec_obj[slot]];
+    const RecRef r = rec_at(ws, idx, j, &pos);
+    const uint32_t win = rec_win(ws, r);
     double p[4], pt[3];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot];
+    const DevObject& o = S.obj[rec_read(ws, r, p, pt)];
     XYZA col;
     if (shade_record<G>(S, rc, o, p, pt, &col, false) != GRT_OK) return 0u;
-    bool last_in_window = (j + 1 == nr) || (ws.rec_win[slot + n] != win);
-    if (last_in_window && o.kind == GRT_OBJ_VOLUMETRIC_DISC) mask |= 1u << j;
+    bool last_in_window = (j + 1 == nr) || (rec_next_win(ws, idx, j, r) != win);
+    if (last_in_window && o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
+      if (!r.pool) mask |= 1u << j;
+      else pool_jobs++;
+    }
+  }
+  if (pool_jobs) {  // the rare rays with more than GRT_WS_SLOTS candidates: no error, append
+    unsigned long long at = atomicAdd(ws.march, (unsigned long long)pool_jobs);
+    pos = HIT_NIL;
+    for (uint32_t j = GRT_WS_SLOTS; j < nr; ++j) {
+      const RecRef r = rec_at(ws, idx, j, &pos);
+      bool last_in_window = (j + 1 == nr) || (rec_next_win(ws, idx, j, r) != rec_win(ws, r));
+      if (last_in_window && S.obj[ws.pool->obj[r.s]].kind == GRT_OBJ_VOLUMETRIC_DISC)
+        ws.jobs[at++] = JOB_POOL | (idx << 31) | r.s;
+    }
   }
   return mask;
 }
@@ -2256,45 +2350,58 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     for (uint32_t m = mask; m; m &= m - 1u) ws.jobs[pos++] = (idx << 8) | (uint64_t)__ffs(m) - 1u;
     return;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(ws.pool->count + 1, *ws.pool->count);
   if (idx >= n_live) return;
   int status = ws.status[idx];
   int stop = ws.stop[idx];
   uint32_t steps = ws.steps[idx];
   const XYZA fail{0.0, 0.0, 0.0, 1.0};
   if (status != GRT_OK) {  // integrate error: reference default pixel (raytracer.rs:204-210)
-    write_out(out, idx, fail, GRT_CLASS_ESCAPED, status, stop, steps);
+    write_out(out, idx, fail, GRT_CLASS_ESCAPED, status, stop, steps, 0u);
     return;
   }
   RayConst rc{ws.rc[idx], ws.rc[n + idx], ws.rc[2 * n + idx], ws.rc[3 * n + idx]};
-  uint32_t nrec = ws.nrec[idx];
-  uint32_t nr = nrec < GRT_MAX_HITS ? nrec : GRT_MAX_HITS;
-  XYZA hits[GRT_MAX_HITS];
-  int nh = 0;
+  bool lost;
+  const uint32_t nr = rec_count(ws, idx, &lost);
+  // window-nearest hits: the first ones in registers, the later ones (pool records of
+  // rays with more than GRT_WS_SLOTS candidates) next to their record, linked backwards
+  XYZA hits[GRT_WS_SLOTS];
+  uint32_t nh = 0, n_pool_hits = 0, pos = HIT_NIL, last_pool_hit = HIT_NIL;
   double opacity = 0.0;
   for (uint32_t j = 0; j < nr; ++j) {
-    const uint64_t slot = (uint64_t)j * n + idx;
-    uint32_t win = ws.rec_win[slot];
-    const DevObject& o = S.obj[ws.rec_obj[slot]];
+    const RecRef r = rec_at(ws, idx, j, &pos);
+    const uint32_t win = rec_win(ws, r);
     double p[4], pt[3];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[(uint64_t)q * GRT_MAX_HITS * n + slot];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[(uint64_t)q * GRT_MAX_HITS * n + slot];
+    const DevObject& o = S.obj[rec_read(ws, r, p, pt)];
     XYZA col{0.0, 0.0, 0.0, 0.0};
     int e = shade_record<G>(S, rc, o, p, pt, &col);
     if (e != GRT_OK) {  // any window error aborts the pixel (scene.rs:146, objects.rs:96-102)
-      write_out(out, idx, fail, GRT_CLASS_ESCAPED, e, stop, steps);
+      write_out(out, idx, fail, GRT_CLASS_ESCAPED, e | (lost ? GRT_FLAG_HIT_OVERFLOW : 0), stop, steps,
+                nh + n_pool_hits);
+      if (lost) atomicAdd(stats + 3, 1ull);
       return;
     }
-    bool last_in_window = (j + 1 == nr) || (ws.rec_win[slot + n] != win);
+    bool last_in_window = (j + 1 == nr) || (rec_next_win(ws, idx, j, r) != win);
     if constexpr (MODE == 2) {
       if (last_in_window && o.kind == GRT_OBJ_VOLUMETRIC_DISC) {
-        const uint64_t MN = (uint64_t)GRT_MAX_HITS * n;
-        col = XYZA{ws.vcol[slot], ws.vcol[MN + slot], ws.vcol[2 * MN + slot], ws.vcol[3 * MN + slot]};
+        const double* vc = r.pool ? ws.pool->vcol : ws.vcol;
+        const uint64_t m = r.pool ? ws.pool->cap : (uint64_t)GRT_WS_SLOTS * n;
+        col = XYZA{vc[r.s], vc[m + r.s], vc[2 * m + r.s], vc[3 * m + r.s]};
       }
     }
     if (last_in_window) {  // the window's nearest hit
-      hits[nh++] = col;
+      if (!r.pool) {
+        hits[nh++] = col;
+      } else {
+        const uint64_t m = ws.pool->cap;
+        ws.pool->hcol[r.s] = col.x;
+        ws.pool->hcol[m + r.s] = col.y;
+        ws.pool->hcol[2 * m + r.s] = col.z;
+        ws.pool->hcol[3 * m + r.s] = col.a;
+        ws.pool->hprev[r.s] = last_pool_hit;
+        last_pool_hit = (uint32_t)r.s;
+        n_pool_hits++;
+      }
       double alpha = rclamp(col.a, 0.0, 1.0);
       opacity = alpha + opacity * (1.0 - alpha);
     }
@@ -2330,13 +2437,18 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     result = blend(result, texture_color(S, S.celestial, 1.0 - u, v, redshift, S.celestial_temperature));
     cls = GRT_CLASS_ESCAPED;
   }
-  for (int k = nh - 1; k >= 0; --k) result = blend(result, hits[k]);
+  // back to front: the pool's hits (the farthest windows), then the first ones
+  for (uint32_t q = last_pool_hit; q != HIT_NIL; q = ws.pool->hprev[q]) {
+    const uint64_t m = ws.pool->cap;
+    result = blend(result, XYZA{ws.pool->hcol[q], ws.pool->hcol[m + q], ws.pool->hcol[2 * m + q], ws.pool->hcol[3 * m + q]});
+  }
+  for (int k = (int)nh - 1; k >= 0; --k) result = blend(result, hits[k]);
   if (opacity >= S.hit_threshold) cls = GRT_CLASS_HIT;
-  if (nrec > GRT_MAX_HITS) {
+  if (lost) {  // the pool was full: candidates past the workspace slots are missing
     status |= GRT_FLAG_HIT_OVERFLOW;
     atomicAdd(stats + 3, 1ull);
   }
-  write_out(out, idx, result, cls, status, stop, steps);
+  write_out(out, idx, result, cls, status, stop, steps, nh + n_pool_hits);
 }
 
 // ------------------------------------------------------------------ launch -------

@@ -87,6 +87,12 @@ struct SubsampleFailures {
   uint64_t* key;      // pixel * spa^2 + stratum
   uint8_t* status;
   uint64_t cap;
+  // with `stop` set, the list also takes the sub-rays without an error that ended on NaN
+  // coordinates or without a terminal event (status 0), with their stop reason and steps
+  uint8_t* stop;
+  uint32_t* steps;
+  const uint8_t* ray_stop;    // the sub-ray trace's stop reasons / step counts
+  const uint32_t* ray_steps;
 };
 hipError_t launch_average(const uint32_t* d_sel_out, const uint32_t* d_sel_px, uint64_t n_sel,
                           const unsigned long long* d_count, uint64_t base, uint32_t spa, const double* d_samples,

@@ -315,7 +315,8 @@ GDEV bool vdisc_no_more_density(const DevObject& o, const V3& p, const V3& rd) {
 }
 
 // ---- march kernel: one lane per job, refilled by wave ballot -----------------------
-// Job = (ray slot << 8) | candidate slot.  Colour goes to ws.vcol at the candidate slot.
+// Job = (ray slot << 8) | candidate slot, colour to ws.vcol at the candidate slot; or
+// JOB_POOL | ray << 31 | pool record, colour to the record's vcol.
 // The per-sample table lookups (temperature LUT of the first volumetric object with one,
 // the blackbody LUT) are binary searches of ~10 dependent loads: staged in LDS (48 KB).
 constexpr uint32_t MARCH_LUT_MAX = 1000;
@@ -351,7 +352,7 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
   const uint64_t n_jobs = ws.march[0];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(ws.march + 3, (unsigned long long)n_jobs);
   const uint64_t n = ws.n;
-  const uint64_t MN = (uint64_t)GRT_MAX_HITS * n;
+  const uint64_t MN = (uint64_t)GRT_WS_SLOTS * n;
   constexpr uint64_t CHUNK = 64;
   uint64_t chunk_next = 0, chunk_end = 0;
   bool active = false, done = false;
@@ -361,7 +362,7 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
   V3 ro{0, 0, 0}, rd{0, 0, 0};
   double d_o = 0.0, exit_d = 0.0, transparency = 1.0, aws = 0.0, awt = 0.0;
   double acc_x = 0.0, acc_y = 0.0, acc_z = 0.0, obs = 0.0, f_pt = 0.0, f_pphi = 0.0;
-  bool cached = false;
+  bool cached = false, pool_job = false;
 
   while (true) {
     bool need = !active && !done;
@@ -382,12 +383,24 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
           done = true;
         } else {
           const uint64_t job = ws.jobs[item];
-          const uint64_t idx = job >> 8;
-          const uint32_t j = (uint32_t)(job & 255u);
-          slot = (uint64_t)j * n + idx;
-          k = ws.rec_obj[slot];
-          ro = V3{ws.rec_pt[slot], ws.rec_pt[MN + slot], ws.rec_pt[2 * MN + slot]};
-          const V3 dir{ws.rec_dir[slot], ws.rec_dir[MN + slot], ws.rec_dir[2 * MN + slot]};
+          pool_job = (job & JOB_POOL) != 0;
+          uint64_t idx;
+          V3 dir;
+          if (!pool_job) {
+            idx = job >> 8;
+            const uint32_t j = (uint32_t)(job & 255u);
+            slot = (uint64_t)j * n + idx;
+            k = ws.rec_obj[slot];
+            ro = V3{ws.rec_pt[slot], ws.rec_pt[MN + slot], ws.rec_pt[2 * MN + slot]};
+            dir = V3{ws.rec_dir[slot], ws.rec_dir[MN + slot], ws.rec_dir[2 * MN + slot]};
+          } else {  // a candidate past the workspace slots (HitPool record)
+            idx = (job & ~JOB_POOL) >> 31;
+            slot = job & 0x7fffffffull;
+            const uint64_t m = ws.pool->cap;
+            k = ws.pool->obj[slot];
+            ro = V3{ws.pool->pt[slot], ws.pool->pt[m + slot], ws.pool->pt[2 * m + slot]};
+            dir = V3{ws.pool->dir[slot], ws.pool->dir[m + slot], ws.pool->dir[2 * m + slot]};
+          }
           const double dn = vnorm(dir);  // .normalize()
           rd = V3{dir.x / dn, dir.y / dn, dir.z / dn};
           obs = ws.rc[idx];
@@ -480,8 +493,10 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
         col[2] = acc_z;
         col[3] = physical_opacity * texture_alpha;
       }
+      double* vc = pool_job ? ws.pool->vcol : ws.vcol;
+      const uint64_t m = pool_job ? ws.pool->cap : MN;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ws.vcol[q * MN + slot] = col[q];
+      for (int q = 0; q < 4; ++q) vc[q * m + slot] = col[q];
       active = false;
     }
   }

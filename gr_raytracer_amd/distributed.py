@@ -272,8 +272,9 @@ def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int
 
     failures: optional _lib.SubsampleFailures filled with this rank's failed sub-samples
     (frame pixel indices; the reference logs them, raytracer.rs:357-362).  report:
-    optional dict that receives this rank's 1-spp "status" (device u8, local rows) and
-    the local rows' "frame_rows" (the errors the reference logs at raytracer.rs:232-239).
+    optional dict that receives this rank's 1-spp "status", "stop" and "steps" (device
+    tensors, local rows) and the local rows' "frame_rows" (the errors the reference logs
+    at raytracer.rs:232-239, the NaN / no-terminal-event rays of scene.rs:178-202).
     cfg: grt_adaptive_config (default: the scene's own).  `enabled` false and no mask:
     plain 1-spp frame (render_section_to_cie_buffer_raw).  Returns on dst
     (xyza64 (n,4) f64, class u8, status u8, n_supersampled over all ranks) or, with
@@ -300,11 +301,19 @@ def render_frame_adaptive(scene, rank: int, world: int, cfg=None, band_rows: int
         stats = torch.zeros(4, dtype=torch.int64, device=dev)
     sh = L.RowShard(band_rows, rank, world)
     lib = L.lib()
+    steps = stop = None
+    if report is not None:  # what color_of_ray's NaN / no-terminal-event lines need (scene.rs:178-202)
+        steps = torch.empty(n_local, dtype=torch.int32, device=dev)
+        stop = torch.empty(n_local, dtype=torch.uint8, device=dev)
     L.check(lib.grt_render_shard_async(scene._s, device, stream.cuda_stream, C.byref(sh), xyza.data_ptr(),
-                                       cls.data_ptr(), status.data_ptr(), xyza64.data_ptr(), None, None,
+                                       cls.data_ptr(), status.data_ptr(), xyza64.data_ptr(),
+                                       steps.data_ptr() if steps is not None else None,
+                                       stop.data_ptr() if stop is not None else None,
                                        stats.data_ptr()), "grt_render_shard_async")
     if report is not None:
         report["status"] = status
+        report["stop"] = stop
+        report["steps"] = steps
         report["frame_rows"] = shard_frame_rows(rows, band_rows, rank, world)
     n_sel = torch.zeros(1, dtype=torch.int64)
     with torch.cuda.stream(stream):

@@ -30,6 +30,22 @@ ERROR_NAMES = {1: "IntegrationError(MaxStepsReached)", 2: "NoCircularOrbitPossib
                4: "NonFiniteRadius"}
 
 
+def _log(msg: str) -> None:
+    """One log line in one write(2): lines of ranks that share a stderr pipe do not interleave."""
+    os.write(2, (msg + "\n").encode())
+
+
+def log_ray_event(row: int, col: int, stop: int, accepted: int) -> None:
+    """scene.rs:178-183 / :196-202 for an error-free ray that ended on NaN coordinates or
+    without a terminal event (Ray's Debug form cut to its pixel; steps.len() = accepted + 1)."""
+    if stop == 3:  # StopReason::CoordinateIsNan
+        _log(f"[render_dist] ERROR Ray hit NaN coordinates: Ray {{ row: {row}, col: {col}, .. }} with {accepted + 1} "
+              "steps.")
+    elif stop == 0:  # no stop reason
+        _log(f"[render_dist] ERROR Ray did not hit anything: Ray {{ row: {row}, col: {col}, .. }} at Some(Step {{ .. }}) "
+              f"with {accepted + 1} steps.")
+
+
 def _csv(n: int, conv=float):
     def parse(v: str):
         parts = v.split(",")
@@ -131,24 +147,56 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         fail_cap = 1 << 20
         f_pix, f_smp, f_st = np.zeros(fail_cap, np.uint32), np.zeros(fail_cap, np.uint32), np.zeros(fail_cap, np.uint8)
-        fails = L.SubsampleFailures(fail_cap, L.ptr(f_pix, C.c_uint32), L.ptr(f_smp, C.c_uint32),
-                                    L.ptr(f_st, C.c_uint8), 0)
-        report = {}
-        out = render_frame_adaptive(scene, rank, world, band_rows=a.band_rows, device=device, stats=stats,
-                                    sampling_mask_xyza=mask, tone_mapping=None if want_f64 else tone,
-                                    failures=C.byref(fails), report=report)
-        torch.cuda.synchronize()
+        f_stop, f_steps = np.zeros(fail_cap, np.uint8), np.zeros(fail_cap, np.uint32)
+        cfg = scene.adaptive
+        supersampled = bool(cfg.enabled) or mask is not None
+        if supersampled and rank == 0:  # raytracer.rs:264-267
+            _log(f"[render_dist] INFO Rendering section from (0, 0) to ({scene.rows}, {scene.cols}) with supersampling")
+        for attempt in range(2):
+            fails = L.SubsampleFailures(fail_cap, L.ptr(f_pix, C.c_uint32), L.ptr(f_smp, C.c_uint32),
+                                        L.ptr(f_st, C.c_uint8), 0, L.ptr(f_stop, C.c_uint8), L.ptr(f_steps, C.c_uint32))
+            report = {}
+            stats.zero_()
+            out = render_frame_adaptive(scene, rank, world, band_rows=a.band_rows, device=device, stats=stats,
+                                        sampling_mask_xyza=mask, tone_mapping=None if want_f64 else tone,
+                                        failures=C.byref(fails), report=report)
+            torch.cuda.synchronize()
+            # a device hit pool too small for some ray's candidates (grt_hit_pool_reserve):
+            # every rank grows its pool and the frame is traced again, complete
+            lost = stats[3:4].clone() if dist.get_backend() != "gloo" else stats[3:4].cpu()
+            dist.all_reduce(lost)
+            if int(lost[0]) == 0:
+                break
+            if rank == 0:
+                _log(f"[render_dist] WARN {int(lost[0])} pixels lost hit candidates (device hit pool full); "
+                      "growing the pool and tracing again")
+            L.check(L.lib().grt_hit_pool_reserve(scene._s, device, 0, None), "grt_hit_pool_reserve")
         t_render = time.perf_counter() - t0
-        # raytracer.rs:232-239 and :357-362: each rank logs its own pixels' failures
+        # each rank logs its own pixels, in pixel order (the reference logs from its parallel loop):
+        # raytracer.rs:232-239 the failed pixels; scene.rs:178-183 / :196-202 the error-free rays that
+        # ended on NaN coordinates or without a terminal event (steps.len() counts the initial step)
         st_local = report["status"].cpu().numpy().reshape(-1, scene.cols)
-        for li, fi in zip(*np.nonzero(st_local & 0x7F)):
-            print(f"[render_dist] ERROR Unable to compute color for ray at pixel ({fi}, "
-                  f"{report['frame_rows'][li]}): {ERROR_NAMES.get(int(st_local[li, fi] & 0x7F), 'Unknown')}",
-                  file=sys.stderr)
-        for k in range(min(int(fails.count), fail_cap)):
-            row, col = divmod(int(f_pix[k]), scene.cols)
-            print(f"[render_dist] ERROR Unable to compute color for ray at pixel ({col}, {row}): "
-                  f"{ERROR_NAMES.get(int(f_st[k]), 'Unknown')}", file=sys.stderr)
+        stop_local = report["stop"].cpu().numpy().reshape(-1, scene.cols)
+        steps_local = report["steps"].cpu().numpy().reshape(-1, scene.cols)
+        for li, fi in zip(*np.nonzero((st_local & 0x7F) | np.isin(stop_local, (L.STOP_NAN, L.STOP_NONE)))):
+            row = report["frame_rows"][li]
+            if st_local[li, fi] & 0x7F:
+                _log(f"[render_dist] ERROR Unable to compute color for ray at pixel ({fi}, {row}): "
+                      f"{ERROR_NAMES.get(int(st_local[li, fi] & 0x7F), 'Unknown')}")
+            else:
+                log_ray_event(row, fi, int(stop_local[li, fi]), int(steps_local[li, fi]))
+        if supersampled and mask is None:  # raytracer.rs:325 (rank 0: the frame's count), then the sub-rays
+            if rank == 0:
+                _log(f"[render_dist] INFO Supersampling {out[-1]} pixels")
+            for k in range(min(int(fails.count), fail_cap)):
+                row, col = divmod(int(f_pix[k]), scene.cols)
+                if f_st[k]:
+                    _log(f"[render_dist] ERROR Unable to compute color for ray at pixel ({col}, {row}): "
+                          f"{ERROR_NAMES.get(int(f_st[k]), 'Unknown')}")
+                else:
+                    log_ray_event(row, col, int(f_stop[k]), int(f_steps[k]))
+        if supersampled and rank == 0:  # raytracer.rs:313-316
+            _log(f"[render_dist] INFO Finished rendering section from (0, 0) to ({scene.rows}, {scene.cols})")
         if dist.get_backend() == "gloo":
             host = stats.cpu()
             dist.all_reduce(host)
@@ -177,10 +225,9 @@ def main(argv=None) -> int:
             rgb = np.ascontiguousarray(rgb_t.cpu().numpy())
             L.check(L.lib().grt_write_png_rgb(a.filename.encode(), L.ptr(rgb, C.c_uint8), w, h), "grt_write_png_rgb")
         steps = int(totals[0])
-        print(f"[render_dist] {world} GPU(s): {int(totals[2])} rays, {steps} accepted steps, {int(totals[1])} attempts, "
-              f"{n_sel} supersampled pixels, frame {t_render:.3f} s ({steps / t_render:.3e} steps/s)",
-              file=sys.stderr)
-        print(f"saved image to {a.filename}\nElapsed time: {time.perf_counter() - t_start:.3f} s", file=sys.stderr)
+        _log(f"[render_dist] {world} GPU(s): {int(totals[2])} rays, {steps} accepted steps, {int(totals[1])} attempts, "
+              f"{n_sel} supersampled pixels, frame {t_render:.3f} s ({steps / t_render:.3e} steps/s)")
+        _log(f"saved image to {a.filename}\nElapsed time: {time.perf_counter() - t_start:.3f} s")
         return 0
     finally:
         dist.destroy_process_group()

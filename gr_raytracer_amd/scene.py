@@ -115,6 +115,7 @@ class RenderResult:
     xyza64: Optional[np.ndarray] = None
     steps: Optional[np.ndarray] = None
     stop_reason: Optional[np.ndarray] = None
+    hits: Optional[np.ndarray] = None  # uint32 (n,): windows with an intersection (scene.rs:141-152)
     stats: dict = field(default_factory=dict)
 
 
@@ -127,6 +128,12 @@ class SectionResult:
     stats: dict
     n_failed_subsamples: int
     failed_subsamples: np.ndarray  # (m, 3) uint32: section pixel, stratum, status (m <= capacity)
+    # log_events=True: the 1-spp rays' stop reasons and accepted steps, and the supersample
+    # sub-rays that ended on NaN coordinates or without a terminal event (no error):
+    # (k, 4) uint32 section pixel, stratum, stop reason, accepted steps (scene.rs:178-202)
+    stop: Optional[np.ndarray] = None
+    steps: Optional[np.ndarray] = None
+    subsample_events: Optional[np.ndarray] = None
 
 
 def _stats_dict(st: L.Stats) -> dict:
@@ -189,7 +196,9 @@ class Scene:
             res.xyza64 = np.zeros((n, 4), np.float64)
             res.steps = np.zeros(n, np.uint32)
             res.stop_reason = np.zeros(n, np.uint8)
-            a = L.AuxOut(L.dptr(res.xyza64), L.ptr(res.steps, C.c_uint32), L.ptr(res.stop_reason, C.c_uint8))
+            res.hits = np.zeros(n, np.uint32)
+            a = L.AuxOut(L.dptr(res.xyza64), L.ptr(res.steps, C.c_uint32), L.ptr(res.stop_reason, C.c_uint8),
+                         L.ptr(res.hits, C.c_uint32))
         st = L.Stats()
         L.check(L.lib().grt_render_pixels(self._s, device, row0, col0, rows, cols,
                                           C.byref(off) if off is not None else None,
@@ -208,7 +217,9 @@ class Scene:
         a = None
         if aux:
             res.xyza64, res.steps, res.stop_reason = np.zeros((n, 4)), np.zeros(n, np.uint32), np.zeros(n, np.uint8)
-            a = L.AuxOut(L.dptr(res.xyza64), L.ptr(res.steps, C.c_uint32), L.ptr(res.stop_reason, C.c_uint8))
+            res.hits = np.zeros(n, np.uint32)
+            a = L.AuxOut(L.dptr(res.xyza64), L.ptr(res.steps, C.c_uint32), L.ptr(res.stop_reason, C.c_uint8),
+                         L.ptr(res.hits, C.c_uint32))
         st = L.Stats()
         L.check(L.lib().grt_render_shard(self._s, device, C.byref(sh), L.ptr(xyza, C.c_float), L.ptr(cls, C.c_uint8),
                                          L.ptr(status, C.c_uint8), C.byref(a) if a is not None else None,
@@ -226,9 +237,11 @@ class Scene:
 
     def render_section_ex(self, from_row: int = 0, from_col: int = 0, to_row: Optional[int] = None,
                           to_col: Optional[int] = None, adaptive: Optional[L.AdaptiveConfig] = None,
-                          sampling_mask_xyza=None, device: int = 0, failure_capacity: int = 1 << 16):
+                          sampling_mask_xyza=None, device: int = 0, failure_capacity: int = 1 << 16,
+                          log_events: bool = False):
         """render_section plus each pixel's 1-spp status and the failed supersample
-        sub-rays ((pixel, stratum, status), sorted; raytracer.rs:232-239, :357-362)."""
+        sub-rays ((pixel, stratum, status), sorted; raytracer.rs:232-239, :357-362); with
+        log_events, also what color_of_ray's NaN / no-terminal-event log lines need."""
         to_row = self.rows if to_row is None else to_row
         to_col = self.cols if to_col is None else to_col
         n = (to_row - from_row) * (to_col - from_col)
@@ -243,17 +256,29 @@ class Scene:
         fp = np.zeros(failure_capacity, np.uint32)
         fs = np.zeros(failure_capacity, np.uint32)
         fst = np.zeros(failure_capacity, np.uint8)
+        fsp = np.zeros(failure_capacity, np.uint8)
+        fn = np.zeros(failure_capacity, np.uint32)
         fails = L.SubsampleFailures(failure_capacity, L.ptr(fp, C.c_uint32), L.ptr(fs, C.c_uint32),
-                                    L.ptr(fst, C.c_uint8), 0)
+                                    L.ptr(fst, C.c_uint8), 0, L.ptr(fsp, C.c_uint8) if log_events else None,
+                                    L.ptr(fn, C.c_uint32) if log_events else None)
+        stop = np.zeros(n, np.uint8) if log_events else None
+        steps = np.zeros(n, np.uint32) if log_events else None
         L.check(L.lib().grt_render_section_ex(self._s, device, from_row, from_col, to_row, to_col,
                                               C.byref(adaptive or self.adaptive),
                                               L.dptr(mask) if mask is not None else None, L.dptr(out),
                                               L.ptr(cls, C.c_uint8), C.byref(nsel), C.byref(st),
-                                              L.ptr(status, C.c_uint8), C.byref(fails)),
+                                              L.ptr(status, C.c_uint8), C.byref(fails),
+                                              L.ptr(stop, C.c_uint8) if log_events else None,
+                                              L.ptr(steps, C.c_uint32) if log_events else None),
                 "grt_render_section_ex")
         m = min(int(fails.count), failure_capacity)
-        return SectionResult(out, cls, status, int(nsel.value), _stats_dict(st), int(fails.count),
-                             np.stack([fp[:m], fs[:m], fst[:m].astype(np.uint32)], axis=1))
+        rows = np.stack([fp[:m], fs[:m], fst[:m].astype(np.uint32)], axis=1)
+        if not log_events:
+            return SectionResult(out, cls, status, int(nsel.value), _stats_dict(st), int(fails.count), rows)
+        failed = fst[:m] != 0
+        events = np.stack([fp[:m], fs[:m], fsp[:m].astype(np.uint32), fn[:m]], axis=1)[~failed]
+        return SectionResult(out, cls, status, int(nsel.value), _stats_dict(st), int(fails.count) - len(events),
+                             rows[failed], stop, steps, events)
 
     def _trace(self, fn, a, b, width: int, capacity: int, device: int):
         a = np.ascontiguousarray(a, np.float64).reshape(-1, width)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GRT_ABI_VERSION 2
+#define GRT_ABI_VERSION 3
 
 /* ---- enums (values are part of the ABI) -------------------------------------- */
 
@@ -82,7 +82,11 @@ enum grt_status {
   GRT_ERR_NO_CIRCULAR_ORBIT = 2,     /* circular_orbit.rs:93-101                        */
   GRT_ERR_BELOW_RISCO = 3,           /* temperature.rs:204-217                          */
   GRT_ERR_NON_FINITE_RADIUS = 4,     /* temperature.rs:199-202                          */
-  GRT_FLAG_HIT_OVERFLOW = 0x80       /* more than GRT_MAX_HITS intersections on one ray */
+  GRT_FLAG_HIT_OVERFLOW = 0x80       /* the device hit pool was full: this ray's candidates
+                                        past GRT_MAX_HITS are missing.  Only the *_async
+                                        calls can return it (grt_hit_pool_reserve, then
+                                        trace again); the synchronous calls grow the pool
+                                        and trace again by themselves.                   */
 };
 
 /* Stop reason of the integration (integrator.rs:22-27), recorded per pixel. */
@@ -95,6 +99,9 @@ enum grt_stop_reason {
 };
 
 #define GRT_MAX_OBJECTS 8
+/* Window candidates a ray keeps in its fixed workspace slots; any further ones go to a
+ * device-wide hit pool, so every window's intersection reaches the pixel as in the
+ * reference (scene.rs:139-152, :206-210).  An implementation constant, not a limit. */
 #define GRT_MAX_HITS 16
 
 /* ---- POD scene descriptor ------------------------------------------------------ */
@@ -304,7 +311,7 @@ typedef struct grt_stats {
   uint64_t accepted_steps; /* iterations of integrator.rs:100 that produced a step     */
   uint64_t attempts;       /* rkf45_step evaluations (6 RHS each)                      */
   uint64_t rays;
-  uint64_t hit_overflows;
+  uint64_t hit_overflows;  /* pixels flagged GRT_FLAG_HIT_OVERFLOW (0 for the sync calls)     */
   double kernel_ms;        /* hipEvent time of the integration kernel(s)               */
   /* VolumetricDisc raymarches (volumetric_disc.rs:199-328): one per window-nearest
    * volumetric intersection whose colour reaches the composite, and their samples. */
@@ -328,6 +335,9 @@ typedef struct grt_aux_out {
   double* xyza64;       /* 4 doubles per sample: the f64 colour before the f32 cast   */
   uint32_t* steps;      /* accepted steps per sample                                  */
   uint8_t* stop_reason; /* grt_stop_reason per sample                                 */
+  uint32_t* hits;       /* windows with an intersection per sample: intersections.len()
+                           of scene.rs:141-152 before the terminal colour (for a pixel
+                           aborted by a window error, the windows before it)           */
 } grt_aux_out;
 
 int grt_scene_create(const grt_scene_desc* desc, grt_scene** out);
@@ -373,17 +383,25 @@ typedef struct grt_subsample_failures {
   uint32_t* sample;  /* nullable: stratum index stratum_row * spa + stratum_col          */
   uint8_t* status;   /* grt_status of the failed sub-sample ray                         */
   uint64_t count;    /* out                                                             */
+  /* Nullable.  When set, the list also holds the sub-rays that ended without an error
+   * but on NaN coordinates or without a terminal event (status 0, stop GRT_STOP_NAN /
+   * GRT_STOP_NONE), which the reference logs from color_of_ray (scene.rs:178-183,
+   * :196-202); every entry then carries its stop reason and accepted steps.          */
+  uint8_t* stop;
+  uint32_t* steps;   /* nullable */
 } grt_subsample_failures;
 
-/* grt_render_section plus the failed sub-samples (nullable).  The whole section stays
- * on the device between the 1-spp pass and the supersample pass: the luminance floor,
- * the selection, its compaction and count, and the sub-ray launches' sizes are decided
- * there (no host round trip). */
+/* grt_render_section plus the failed sub-samples (nullable) and the 1-spp rays' stop
+ * reasons and accepted steps per section pixel (nullable; the reference's color_of_ray
+ * logs the NaN and no-terminal-event rays, scene.rs:178-183, :196-202).  The whole
+ * section stays on the device between the 1-spp pass and the supersample pass: the
+ * luminance floor, the selection, its compaction and count, and the sub-ray launches'
+ * sizes are decided there (no host round trip). */
 int grt_render_section_ex(grt_scene* scene, int device, uint32_t from_row, uint32_t from_col,
                           uint32_t to_row, uint32_t to_col, const grt_adaptive_config* cfg,
                           const double* sampling_mask_xyza, double* xyza_out, uint8_t* class_out,
                           uint64_t* n_supersampled, grt_stats* stats, uint8_t* status_out,
-                          grt_subsample_failures* failures);
+                          grt_subsample_failures* failures, uint8_t* stop_out, uint32_t* steps_out);
 
 /* Row-band sharding of one frame across GPUs (multi-GPU render).
  * The frame's rows are cut into bands of `band_rows` rows (the last may be short);
@@ -412,6 +430,19 @@ int grt_render_shard(grt_scene* scene, int device, const grt_row_shard* sh, floa
 int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt_row_shard* sh,
                            float* d_xyza, uint8_t* d_class, uint8_t* d_status, double* d_xyza64,
                            uint32_t* d_steps, uint8_t* d_stop, uint64_t* d_stats);
+
+/* The device hit pool that keeps the window candidates past a ray's GRT_MAX_HITS slots
+ * (no reference counterpart: the reference's per-ray Vec grows, scene.rs:139-152).
+ * The pool grows on its own to half the rays of a trace; a trace that needs more flags
+ * the pixels it could not keep (GRT_FLAG_HIT_OVERFLOW, grt_stats.hit_overflows).  The
+ * synchronous calls then grow it and trace again.  After an *_async call whose
+ * d_stats[3] is non-zero, call this with records = 0 (waits for the device, then sizes
+ * the pool for the largest trace since the last call) or with an explicit record count,
+ * and trace again.  *capacity (nullable) returns the pool size in records. */
+int grt_hit_pool_reserve(grt_scene* scene, int device, uint64_t records, uint64_t* capacity);
+/* Smallest pool a trace allocates (default 2^20 records; tests lower it to exercise a
+ * full pool).  Applies to pools allocated or grown afterwards. */
+int grt_set_hit_pool_min(uint64_t records);
 
 /* ---- adaptive supersampling of a frame split across GPUs -------
  * render_section_to_cie_buffer_supersampled (raytracer.rs:257-318) with the frame's

@@ -1656,6 +1656,7 @@ struct Sample {
   int status;
   int stop;
   uint64_t steps;
+  uint32_t hits;  // windows with an intersection (intersections.len() before the terminal colour)
 };
 
 // scene.rs:114-220
@@ -1669,6 +1670,7 @@ static Err color_of_ray(const SceneCtx& S, const Ray& ray, Sample* out, Counters
   cnt->attempts += local.attempts;
   out->steps = local.accepted;
   out->stop = stop;
+  out->hits = 0;
   if (e != OK) return e;
   double observer_energy = g.inner_product(ray.position, S.cam_velocity, ray.momentum);  // redshift.rs:40-43
   FrequencyData freq = ray_frequency_data(S, ray, observer_energy);
@@ -1681,6 +1683,7 @@ static Err color_of_ray(const SceneCtx& S, const Ray& ray, Sample* out, Counters
     if (ie != OK) return ie;
     if (has) {
       intersections.push_back(c);
+      out->hits++;
       double alpha = rust_clamp(c.alpha, 0.0, 1.0);
       object_opacity = alpha + object_opacity * (1.0 - alpha);
     }
@@ -1750,6 +1753,7 @@ static void trace_one(const SceneCtx& S, int64_t row, int64_t col, bool offset, 
     s->status = e;
     s->steps = tmp.steps;
     s->stop = tmp.stop;
+    s->hits = tmp.hits;
   } else {
     *s = tmp;
     s->status = OK;
@@ -1899,7 +1903,7 @@ double oracle_render_pixels(const grt_scene_desc* d, uint32_t row0, uint32_t col
                             const double* odx, const double* ody, const uint32_t* row_list,
                             uint32_t n_row_list, double* xyza, uint8_t* cls, uint8_t* status,
                             uint8_t* stop, uint32_t* steps, int threads, uint64_t* total_accepted,
-                            uint64_t* total_attempts) {
+                            uint64_t* total_attempts, uint32_t* hits) {
   SceneCtx S;
   init_ctx(S, d);
   // Work list: rectangle rows (or an explicit subset of rectangle rows) x cols, or offsets.
@@ -1938,6 +1942,7 @@ double oracle_render_pixels(const grt_scene_desc* d, uint32_t row0, uint32_t col
     if (status) status[i] = (uint8_t)s.status;
     if (stop) stop[i] = (uint8_t)s.stop;
     if (steps) steps[i] = (uint32_t)s.steps;
+    if (hits) hits[i] = s.hits;
   }
   auto t1 = std::chrono::steady_clock::now();
   if (total_accepted) *total_accepted = acc.load();

@@ -36,7 +36,7 @@ def lib():
         L.oracle_render_pixels.restype = _d
         L.oracle_render_pixels.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, _u32p,
                                            _pd, _pd, _u32p, C.c_uint32, _pd, _u8p, _u8p, _u8p, _u32p, C.c_int,
-                                           _u64p, _u64p]
+                                           _u64p, _u64p, _u32p]
         L.oracle_health_pixels.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, _pd, _u8p]
         L.oracle_render_section.restype = C.c_uint64
         L.oracle_render_section.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, _pd, _pd, _u8p,
@@ -107,7 +107,8 @@ def color_of_ray(desc, row, col, offset=None):
 
 
 def render_pixels(desc, row0, col0, rows, cols, threads=8, offsets=None, row_list=None):
-    """Returns dict with xyza (n,4) f64, ray_class, status, stop, steps, wall_s, accepted, attempts."""
+    """Returns dict with xyza (n,4) f64, ray_class, status, stop, steps, hits (windows with an
+    intersection), wall_s, accepted, attempts."""
     if offsets is not None:
         pix = np.ascontiguousarray(offsets[0], np.uint32)
         dx = np.ascontiguousarray(offsets[1], np.float64)
@@ -121,13 +122,14 @@ def render_pixels(desc, row0, col0, rows, cols, threads=8, offsets=None, row_lis
     xyza = np.zeros((n, 4))
     cls, st, stop = np.zeros(n, np.uint8), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
     steps = np.zeros(n, np.uint32)
+    hits = np.zeros(n, np.uint32)
     acc, att = C.c_uint64(), C.c_uint64()
     wall = lib().oracle_render_pixels(_addr(desc), row0, col0, rows, cols, *args,
                                       rl.ctypes.data_as(_u32p) if rl is not None else None,
                                       0 if rl is None else len(rl), _dp(xyza), cls.ctypes.data_as(_u8p),
                                       st.ctypes.data_as(_u8p), stop.ctypes.data_as(_u8p), steps.ctypes.data_as(_u32p),
-                                      threads, C.byref(acc), C.byref(att))
-    return {"xyza": xyza, "ray_class": cls, "status": st, "stop": stop, "steps": steps, "wall_s": wall,
+                                      threads, C.byref(acc), C.byref(att), hits.ctypes.data_as(_u32p))
+    return {"xyza": xyza, "ray_class": cls, "status": st, "stop": stop, "steps": steps, "hits": hits, "wall_s": wall,
             "accepted": acc.value, "attempts": att.value}
 
 

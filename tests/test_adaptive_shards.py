@@ -306,3 +306,58 @@ def test_device_floor_equals_host_floor(grt, gpu, n):
                                                           C.byref(got)), "grt_adaptive_min_luminance_device")
         assert struct.pack("<d", got.value) == struct.pack("<d", want) or (np.isnan(got.value) and np.isnan(want))
 
+
+
+@pytest.mark.gpu
+def test_cli_logs_unterminated_rays_like_the_reference(grt, oracle, gpu, tmp_path):
+    """scene.rs:178-183 / :196-202 and raytracer.rs:325: `grt render` and a 2-rank
+    `render_dist` log every error-free ray that ended without a terminal event ("Ray did not
+    hit anything ... with N steps", N = steps.len() incl. the initial step) or on NaN
+    coordinates, 1-spp and supersample sub-rays alike, and "Supersampling N pixels"; the
+    sets equal the oracle's stop reasons.  max-steps 3000 < the ~15000 steps an escaping
+    ray needs, so most rays end on the budget."""
+    import re
+
+    flags = ["--width=48", "--height=40", "--camera-position=-16.0,0.0,3.5", "--theta=-3.142", "--max-steps=3000",
+             "--config-file", str(SCENES / "schwarzschild.toml"), "--resource-root", str(RESOURCES)]
+    pat = r"Ray (did not hit anything|hit NaN coordinates): Ray \{ row: (\d+), col: (\d+), \.\. \}.* with (\d+) steps\."
+
+    def events(text):
+        return sorted((int(r), int(c), int(n), kind.startswith("hit")) for kind, r, c, n in re.findall(pat, text))
+
+    r = subprocess.run([str(ROOT / "gr_raytracer_amd" / "lib" / "grt"), *flags, "render", "--filename",
+                        str(tmp_path / "o.png")], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    hs = grt.HostScene(str(SCENES / "schwarzschild.toml"), c2_opts(grt, width=48, height=40, max_steps=3000),
+                       str(RESOURCES))
+    ref = oracle.render_pixels(hs.desc, 0, 0, 40, 48, threads=16)
+    want = []
+    for p in np.flatnonzero((ref["status"] == 0) & np.isin(ref["stop"], (0, 3))):
+        want.append((int(p) // 48, int(p) % 48, int(ref["steps"][p]) + 1, bool(ref["stop"][p] == 3)))
+    assert len(want) > 1000
+    ad = hs.adaptive
+    sel, _ = oracle.select_pixels(ref["xyza"], ref["ray_class"], 48, 40, ad)
+    spa = ad.samples_per_axis
+    pix, dx, dy = [], [], []
+    for p in np.flatnonzero(sel):
+        row, col = divmod(int(p), 48)
+        for s in range(spa * spa):
+            ox, oy = oracle.stratified_offset(row, col, s // spa, s % spa, spa)
+            pix.append(p); dx.append(ox); dy.append(oy)
+    sub = oracle.render_pixels(hs.desc, 0, 0, 40, 48, threads=16,
+                               offsets=(np.asarray(pix), np.asarray(dx), np.asarray(dy)))
+    for k in np.flatnonzero((sub["status"] == 0) & np.isin(sub["stop"], (0, 3))):
+        want.append((int(pix[k]) // 48, int(pix[k]) % 48, int(sub["steps"][k]) + 1, bool(sub["stop"][k] == 3)))
+    assert sel.sum() > 0 and len(want) > len(ref["stop"])
+    assert events(r.stderr) == sorted(want)
+    assert re.findall(r"INFO Supersampling (\d+) pixels", r.stderr) == [str(int(sel.sum()))]
+
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    launch = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "gr_raytracer_amd.render_dist",
+              "--backend=gloo", "--band-rows=8"]
+    d = subprocess.run([*launch, *flags, "render", "--filename", str(tmp_path / "d.png")], capture_output=True,
+                       text=True, timeout=240, env=env, cwd=str(ROOT))
+    assert d.returncode == 0, d.stderr[-3000:]
+    assert events(d.stderr) == sorted(want)
+    assert re.findall(r"INFO Supersampling (\d+) pixels", d.stderr) == [str(int(sel.sum()))]

@@ -31,7 +31,7 @@ print(json.dumps(st))
 configs = os.environ.get("CONFIGS", "C2,C3").split(",")
 for name in sys.argv[1:]:
     for cfg in configs:
-        env = dict(os.environ, GRT_LIB=str(ROOT / "variants" / name / "libgrt.so"))
+        env = dict(os.environ, GRT_LIB=str(ROOT / "variants" / name / "libgrt.so"), GRT_LIB_ALLOW_MISSING="1")
         out = subprocess.run([sys.executable, "-c", CODE, cfg], env=env, capture_output=True, text=True, timeout=300)
         if out.returncode != 0:
             print(name, "FAILED", out.stderr[-2000:], flush=True)
