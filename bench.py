@@ -438,8 +438,9 @@ def run_c4(args, rank, world, local_rank, dev):
         "gather_ms": s["gather_ms"],
         "gather_GBps": rows * cols * BYTES_PER_PIXEL_OUT / (s["gather_ms"] * 1e-3) / 1e9 if s["gather_ms"] else None,
         "roofline": roofline("c4", "kerr", s["rank0_accepted"] / s["steps"], s["rank0_attempts"] / s["steps"],
-                             s["per_rank_kernel_ms"][0], n_local, "grt::integrate_kernel<2, false> (Kerr-Schild; "
-                             "events also span the probe pass and shade_kernel<2, 0>), rank 0's shard"),
+                             s["per_rank_kernel_ms"][0], n_local, "grt::integrate_kernel<2, false> + grt::tail_kernel<2, false> "
+                             "(Kerr-Schild; the events also span the probe pass and shade_kernel<2, 0>; "
+                             "traffic: the integrate kernel's PMC summary only), rank 0's shard"),
         "cpu_baseline": None,
     }
     if not args.no_cpu_baseline and world == 1:

@@ -28,7 +28,10 @@ int g_blocks_per_cu = 0;
 int g_threads = 256;
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
 long long g_tail = -1;  // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
+long long g_early = 0;  // grt_set_early_tail: -1 auto, 0 off (default off until measured), > 0 accepted steps before a ray moves early
+int g_early_cus = 0;     // CUs of the early tail kernel (0: automatic)
 constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
+constexpr uint64_t EARLY_STEPS_AUTO = 100000;  // accepted steps before a ray may move early (automatic mode)
 
 
 int fail(int code, const std::string& msg) {
@@ -59,6 +62,10 @@ struct DeviceCopy {
   int cus = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // calls on one device are serialised
+  // the last stream that enqueued work into the shared scratch below (stream_order)
+  hipEvent_t ev_busy = nullptr;
+  hipStream_t busy_stream = nullptr;
+  bool busy = false;
   // integrate -> shade hand-off buffers, grown on demand (bytes per ray: ~1.1 KB)
   uint64_t ws_cap = 0;
   bool ws_vol = false;  // the arena holds the volumetric arrays
@@ -71,9 +78,17 @@ struct DeviceCopy {
   uint64_t ad_bytes = 0;
   void* ad_mem = nullptr;
   // long-ray hand-off (Kerr-Schild): [0] live, [1] handed off, [2] claim cursor; entries, grow-only
-  unsigned long long* d_tail_ctl = nullptr;
+  unsigned long long* d_tail_ctl = nullptr;  // 16 words (TailList::ctl)
   uint64_t tail_cap = 0;
   unsigned long long* tail_mem = nullptr;
+  // early hand-off: the early list (32-word entries + flags, grow-only), the two CU-masked
+  // streams (integrate / early tail kernel) and their events; split_cus = the early CU count
+  // the streams were made for (-1: CU masks unavailable on this device)
+  uint64_t early_cap = 0;
+  void* early_mem = nullptr;
+  int split_cus = 0;
+  hipStream_t s_int = nullptr, s_early = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_int = nullptr, ev_early = nullptr;
   // hit pool: window candidates past a ray's GRT_WS_SLOTS workspace slots, grow-only
   uint64_t pool_cap = 0;
   bool pool_vol = false;
@@ -107,6 +122,22 @@ int ensure_pool(DeviceCopy& dc, uint64_t want) {
   }
   dc.pool_cap = want;
   dc.pool_vol = dc.vol;
+  return 0;
+}
+
+// The scratch of a device (workspace, hit pool, tile order, tail list, adaptive arena) is
+// one grow-only set per device and every call carves it from offset 0.  An async call
+// on another stream than the previous one first waits for that stream's work in it
+// (one event), so two streams never run in the same scratch at once; the call then
+// records the event on its own stream (stream_done).
+int stream_order(DeviceCopy& dc, hipStream_t st) {
+  if (dc.busy && dc.busy_stream != st) HIP_TRY(hipStreamWaitEvent(st, dc.ev_busy, 0));
+  return 0;
+}
+int stream_done(DeviceCopy& dc, hipStream_t st) {
+  HIP_TRY(hipEventRecord(dc.ev_busy, st));
+  dc.busy_stream = st;
+  dc.busy = true;
   return 0;
 }
 
@@ -411,9 +442,9 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   dc.d_counter = (unsigned long long*)p;
   dc.d_stats = dc.d_counter + 1;
   dc.d_march = dc.d_counter + 8;
-  HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&p, 16 * sizeof(unsigned long long)));
   dc.allocations.push_back(p);
-  HIP_TRY(hipMemset(p, 0, 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(p, 0, 16 * sizeof(unsigned long long)));
   dc.d_tail_ctl = (unsigned long long*)p;
   HIP_TRY(hipMalloc(&p, sizeof(grt::HitPool)));
   dc.allocations.push_back(p);
@@ -427,6 +458,7 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   (void)kfn;
   HIP_TRY(hipEventCreate(&dc.ev0));
   HIP_TRY(hipEventCreate(&dc.ev1));
+  HIP_TRY(hipEventCreateWithFlags(&dc.ev_busy, hipEventDisableTiming));
   (void)occ;
   dc.ready = true;
   return 0;
@@ -536,10 +568,90 @@ int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList*
   return 0;
 }
 
+// The early list for n output slots: 32-word entries (two cache lines each) + a flag per
+// entry.  Grow-only.
+int early_list(DeviceCopy& dc, uint64_t n, grt::TailList* tl) {
+  const uint64_t entry_bytes = 32 * sizeof(unsigned long long);
+  if (n > dc.early_cap || !dc.early_mem) {
+    if (dc.early_mem) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(dc.early_mem);
+      dc.early_mem = nullptr;
+    }
+    dc.early_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(n, 1 << 16);
+    HIP_TRY(hipMalloc(&dc.early_mem, cap * entry_bytes + cap * sizeof(unsigned int) + 256));
+    dc.early_cap = cap;
+  }
+  tl->est = (unsigned long long*)dc.early_mem;
+  tl->eready = (unsigned int*)((char*)dc.early_mem + dc.early_cap * entry_bytes);
+  tl->early_cap = n;
+  return 0;
+}
+
+// CU mask of `k` early CUs spread over the XCDs and shader engines whatever the order of
+// the mask's bits (XCD-major or XCD-interleaved): bit j * (cus / k) + j % 8.
+static void early_cu_mask(int cus, int k, bool early, std::vector<uint32_t>* mask) {
+  mask->assign((cus + 31) / 32, 0u);
+  std::vector<char> pick(cus, 0);
+  for (int j = 0; j < k; ++j) pick[(j * (cus / k) + j % 8) % cus] = 1;
+  for (int c = 0; c < cus; ++c)
+    if ((pick[c] != 0) == early) (*mask)[c / 32] |= 1u << (c % 32);
+}
+
+// Decide the early hand-off of one trace and make its streams: returns the early CU
+// count (0: not used) or a negative errno.  Kerr-Schild rectangle traces (frames and
+// row shards) without volumetric objects, when rays may run far past an escaping ray's
+// length (max_steps >= 2^18), with the long-ray hand-off on.
+int early_split(const grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, grt::TailList& tl, grt::EarlySplit* es) {
+  tl.early_steps = 0;
+  tl.est = nullptr;
+  tl.eready = nullptr;
+  tl.early_cap = 0;
+  tl.int_waves = 0;
+  if (g_early == 0 || !tl.cap || dc.vol || wl.pixel_index || wl.n_live || s->desc.geometry != GRT_GEOM_KERR)
+    return 0;
+  if (g_early < 0 && s->desc.max_steps < (1ull << 18)) return 0;
+  const int k = g_early_cus > 0 ? g_early_cus : std::max(8, dc.cus / 16);
+  if (k >= dc.cus || dc.split_cus < 0) return 0;
+  if (dc.split_cus != k) {
+    if (dc.s_int) (void)hipStreamDestroy(dc.s_int);
+    if (dc.s_early) (void)hipStreamDestroy(dc.s_early);
+    dc.s_int = dc.s_early = nullptr;
+    dc.split_cus = 0;
+    std::vector<uint32_t> m_int, m_early;
+    early_cu_mask(dc.cus, k, false, &m_int);
+    early_cu_mask(dc.cus, k, true, &m_early);
+    if (hipExtStreamCreateWithCUMask(&dc.s_int, (uint32_t)m_int.size(), m_int.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&dc.s_early, (uint32_t)m_early.size(), m_early.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      if (dc.s_int) (void)hipStreamDestroy(dc.s_int);
+      dc.s_int = dc.s_early = nullptr;
+      dc.split_cus = -1;  // no CU masks here: every trace runs without the early hand-off
+      return 0;
+    }
+    if (!dc.ev_fork) {
+      HIP_TRY(hipEventCreateWithFlags(&dc.ev_fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&dc.ev_int, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&dc.ev_early, hipEventDisableTiming));
+    }
+    dc.split_cus = k;
+  }
+  tl.early_steps = g_early > 0 ? (uint64_t)g_early : EARLY_STEPS_AUTO;
+  es->s_int = dc.s_int;
+  es->s_early = dc.s_early;
+  es->fork = dc.ev_fork;
+  es->int_done = dc.ev_int;
+  es->early_done = dc.ev_early;
+  es->early_blocks = k * GRT_TAIL_WAVES;
+  return k;
+}
+
 // Enqueue one trace over `wl` on `stream`; counters are zeroed first.
 int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, const grt::Outputs& o,
                   unsigned long long* d_stats, hipStream_t stream) {
   grt::WorkList wl = wl_in;
+  if (int rc0 = stream_order(dc, stream)) return rc0;
   if (schedule_wanted(s, wl)) {
     int rc0 = enqueue_tile_order(s, dc, wl, stream, &wl.tile_order);
     if (rc0) return rc0;
@@ -573,10 +685,22 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   int tail_blocks = 0;
   rc = tail_list(s, dc, blocks * (uint64_t)threads, &tl, &tail_blocks);
   if (rc) return rc;
-  if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 8 * sizeof(unsigned long long), stream));
+  if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 16 * sizeof(unsigned long long), stream));
+  grt::EarlySplit es;
+  const int early_cus = early_split(s, dc, wl, tl, &es);
+  if (early_cus < 0) return early_cus;
+  if (early_cus > 0) {
+    // the integrate kernel runs on the other CUs
+    blocks = (int)std::min<uint64_t>(max_blocks, (uint64_t)(dc.cus - early_cus) * 2 *
+                                                     grt::integrate_waves(s->desc.geometry, dc.vol));
+    tl.int_waves = (uint64_t)blocks * (uint64_t)((threads + 63) / 64);
+    tail_blocks = (dc.cus - early_cus) * GRT_TAIL_WAVES;  // the second early kernel, on the integrate CUs
+    if ((rc = early_list(dc, n_out, &tl))) return rc;
+    HIP_TRY(hipMemsetAsync(tl.eready, 0, n_out * sizeof(unsigned int), stream));
+  }
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
-                            dc.vol, tl, tail_blocks, stream));
-  return 0;
+                            dc.vol, tl, tail_blocks, stream, early_cus > 0 ? &es : nullptr));
+  return stream_done(dc, stream);
 }
 
 struct DevBuf {
@@ -661,20 +785,68 @@ int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double t
   DeviceCopy& dc = *scene->devices[device];
   std::lock_guard<std::mutex> lock(dc.mu);
   HIP_TRY(hipSetDevice(device));
-  unsigned long long v[8];
+  unsigned long long v[16];
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(v, dc.d_tail_ctl, sizeof(v), hipMemcpyDeviceToHost));
   *handed_off = v[1];
+  const bool split = v[8] != 0 || v[9] != 0;  // the last trace ran with the early hand-off
   if (timeline_s) {  // s_memrealtime ticks at 100 MHz
     auto since = [&](unsigned long long t) { return (t && v[3]) ? (double)(long long)(t - v[3]) * 1e-8 : 0.0; };
     timeline_s[0] = since(v[4]);
     timeline_s[1] = since(v[5]);
-    timeline_s[2] = since(v[6]);
+    timeline_s[2] = since(split ? v[12] : v[6]);
+  }
+  if (split && capacity && dc.early_mem) {  // the handed-off rays are in the early list
+    const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(v[8], dc.early_cap), capacity);
+    std::vector<unsigned long long> ent(n * 32);
+    HIP_TRY(hipMemcpy(ent.data(), dc.early_mem, n * 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < n; ++k) {
+      if (slot) slot[k] = ent[k * 32 + 14];
+      if (step) step[k] = ent[k * 32 + 13];
+    }
+    return 0;
   }
   const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(v[1], dc.tail_cap), capacity);
   if (n && dc.tail_mem) {
     if (slot) HIP_TRY(hipMemcpy(slot, dc.tail_mem + 14 * dc.tail_cap, n * 8, hipMemcpyDeviceToHost));
     if (step) HIP_TRY(hipMemcpy(step, dc.tail_mem + 13 * dc.tail_cap, n * 8, hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+int grt_set_early_tail(long long steps, int cus) {
+  if (steps < -1) return fail(-EINVAL, "early hand-off threshold must be -1 (auto), 0 (off) or a step count");
+  if (cus < 0 || cus > 4096) return fail(-EINVAL, "early tail CU count must be 0 (auto) or a CU count");
+  g_early = steps;
+  g_early_cus = cus;
+  return 0;
+}
+
+int grt_early_report(grt_scene* scene, int device, uint64_t* handed_early, uint64_t* handed_final,
+                     double* early_end_s, int* cus, uint64_t early_steps[2]) {
+  if (!scene || !handed_early) return fail(-EINVAL, "null argument");
+  *handed_early = 0;
+  if (handed_final) *handed_final = 0;
+  if (early_end_s) *early_end_s = 0.0;
+  if (cus) *cus = 0;
+  if (early_steps) early_steps[0] = early_steps[1] = 0;
+  if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
+    return 0;
+  DeviceCopy& dc = *scene->devices[device];
+  std::lock_guard<std::mutex> lock(dc.mu);
+  HIP_TRY(hipSetDevice(device));
+  unsigned long long v[16];
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(v, dc.d_tail_ctl, sizeof(v), hipMemcpyDeviceToHost));
+  if (v[13]) return fail(-EIO, "early tail kernel watchdog: the integrate kernel did not finish");
+  // [8] counts every early-list entry; [1] the final hand-off's share of them
+  *handed_early = v[8] >= v[1] ? v[8] - v[1] : 0;
+  if (handed_final) *handed_final = v[1];
+  if (early_end_s && v[12] && v[3]) *early_end_s = (double)(long long)(v[12] - v[3]) * 1e-8;
+  if (cus) *cus = dc.split_cus > 0 ? dc.split_cus : 0;
+  if (early_steps) {
+    early_steps[0] = v[14];
+    early_steps[1] = v[15];
   }
   return 0;
 }
@@ -731,6 +903,12 @@ int grt_scene_destroy(grt_scene* s) {
     if (dc->pool_mem) (void)hipFree(dc->pool_mem);
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
+    if (dc->ev_busy) (void)hipEventDestroy(dc->ev_busy);
+    for (hipEvent_t e : {dc->ev_fork, dc->ev_int, dc->ev_early})
+      if (e) (void)hipEventDestroy(e);
+    if (dc->s_int) (void)hipStreamDestroy(dc->s_int);
+    if (dc->s_early) (void)hipStreamDestroy(dc->s_early);
+    if (dc->early_mem) (void)hipFree(dc->early_mem);
     delete dc;
   }
   delete s;
@@ -999,6 +1177,7 @@ static int ad_reserve(DeviceCopy& dc, uint64_t bytes) {
 }
 
 constexpr uint64_t SUB_CHUNK = 1ull << 21;  // sub-rays per supersample trace launch
+uint64_t g_sub_chunk = SUB_CHUNK;            // grt_set_sub_chunk (tests force several chunks)
 
 // Buffers of the supersample pass over at most n_max selected pixels.
 struct SuperBufs {
@@ -1012,7 +1191,7 @@ struct SuperBufs {
   unsigned long long* live = nullptr;
   void carve(AdArena& A, uint64_t n_max, uint32_t spa) {
     per = spa * spa;
-    chunk_pix = std::max<uint64_t>(1, std::min<uint64_t>(n_max, SUB_CHUNK / per));
+    chunk_pix = std::max<uint64_t>(1, std::min<uint64_t>(n_max, g_sub_chunk / per));
     n_chunks = (uint32_t)((n_max + chunk_pix - 1) / chunk_pix);
     cap = chunk_pix * per;
     pix = (uint32_t*)A.take(cap * 4);
@@ -1031,7 +1210,7 @@ struct SuperBufs {
 // supersample (raytracer.rs:320-384) over a selection that lives on the device: entries
 // j < *d_count <= n_max of sel_px (pixel index in the rect row0/col0/rows/cols: camera
 // ray and jitter hash) and sel_out (index into d_out64).  The sub-rays go through the
-// trace in chunks of SUB_CHUNK; the integrate / shade kernels read each chunk's live
+// trace in chunks of g_sub_chunk; the integrate / shade kernels read each chunk's live
 // count from the device, so nothing waits for the host between the passes.
 static int enqueue_supersample(grt_scene* s, DeviceCopy& dc, hipStream_t st, const SuperBufs& B, uint32_t row0,
                         uint32_t col0, uint32_t rows, uint32_t cols, const uint32_t* sel_px, const uint32_t* sel_out,
@@ -1345,6 +1524,12 @@ int grt_render_shard(grt_scene* s, int device, const grt_row_shard* sh, float* x
   return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
 }
 
+int grt_set_sub_chunk(uint64_t sub_rays) {
+  if (sub_rays > (1ull << 31)) return fail(-EINVAL, "sub-ray chunk larger than 2^31");
+  g_sub_chunk = sub_rays ? sub_rays : SUB_CHUNK;
+  return 0;
+}
+
 int grt_set_hit_pool_min(uint64_t records) {
   if (records == 0 || records > POOL_MAX) return fail(-EINVAL, "hit pool minimum must be in [1, 2^31)");
   g_pool_min = records;
@@ -1442,6 +1627,7 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
     AdArena A{(char*)dc->ad_mem, 0};
     carve(A);
   }
+  if ((rc = stream_order(*dc, st))) return rc;
   HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, st));
   // collect_pixels_to_supersample (raytracer.rs:386-458) over this shard's pixels, with
   // the whole frame's 1-spp buffer as the neighbourhood
@@ -1468,6 +1654,7 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
       return rc;
   }
   if (d_n_supersampled) HIP_TRY(hipMemcpyAsync(d_n_supersampled, d_cnt, 8, hipMemcpyDeviceToDevice, st));
+  if ((rc = stream_done(*dc, st))) return rc;
   if (failures) {
     unsigned long long cnt[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
@@ -1521,8 +1708,9 @@ int grt_adaptive_floor_device(grt_scene* s, int device, void* stream, const doub
   size_t bytes = 0;
   HIP_TRY(grt::luminance_floor_device(d_y, stride, n, floor_index(n), nullptr, &bytes, nullptr, st));
   if ((rc = ad_reserve(*dc, bytes))) return rc;
+  if ((rc = stream_order(*dc, st))) return rc;
   HIP_TRY(grt::luminance_floor_device(d_y, stride, n, floor_index(n), dc->ad_mem, &bytes, d_min_lum, st));
-  return 0;
+  return stream_done(*dc, st);
 }
 
 }  // extern "C"

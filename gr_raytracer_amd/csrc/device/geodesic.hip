@@ -1444,9 +1444,9 @@ struct LoopState {
   int retries;
   bool c_valid;
 };
-GDEV void tail_save(const TailList& tl, uint64_t e, const LoopState& s) {
-  unsigned long long* w = tl.st + e;
-  const uint64_t m = tl.cap;
+// Entry e of an entry arena `st` of m entries ([16][m] words: TailList::st / est).
+GDEV void tail_save(unsigned long long* st, uint64_t m, uint64_t e, const LoopState& s) {
+  unsigned long long* w = st + e;
 #pragma unroll
   for (int k = 0; k < 8; ++k) w[k * m] = (unsigned long long)__double_as_longlong(s.y[k]);
 #pragma unroll
@@ -1458,9 +1458,8 @@ GDEV void tail_save(const TailList& tl, uint64_t e, const LoopState& s) {
   w[15 * m] = (unsigned long long)s.nrec | ((unsigned long long)(uint32_t)s.retries << 32) |
               ((unsigned long long)(s.c_valid ? 1 : 0) << 48);
 }
-GDEV void tail_load(const TailList& tl, uint64_t e, LoopState& s) {
-  const unsigned long long* w = tl.st + e;
-  const uint64_t m = tl.cap;
+GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopState& s) {
+  const unsigned long long* w = st + e;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s.y[k] = __longlong_as_double((long long)w[k * m]);
 #pragma unroll
@@ -1474,8 +1473,79 @@ GDEV void tail_load(const TailList& tl, uint64_t e, LoopState& s) {
   s.retries = (int)((f >> 32) & 0xffffu);
   s.c_valid = ((f >> 48) & 1u) != 0;
 }
+// Early-list entry e: 32 words (256 B, two whole cache lines of its own) written once per
+// trace with write-through (sc1) stores and published by its eready flag; it carries the
+// per-ray constants and the ray's last hit-pool record too, so the early kernel (another
+// CU, often another XCD, in the same launch) reads nothing of the ray but this entry.
+constexpr uint64_t EARLY_WORDS = 32;
+GDEV void early_save(const TailList& tl, uint64_t e, const LoopState& s, const RayConst& rc, uint32_t pool_last) {
+  unsigned long long* w = tl.est + e * EARLY_WORDS;
+  unsigned long long v[21];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = (unsigned long long)__double_as_longlong(s.y[k]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[8 + k] = (unsigned long long)__double_as_longlong(s.c[k]);
+  v[11] = (unsigned long long)__double_as_longlong(s.h);
+  v[12] = (unsigned long long)__double_as_longlong(s.h_cur);
+  v[13] = s.i;
+  v[14] = s.idx;
+  v[15] = (unsigned long long)s.nrec | ((unsigned long long)(uint32_t)s.retries << 32) |
+          ((unsigned long long)(s.c_valid ? 1 : 0) << 48);
+  v[16] = (unsigned long long)__double_as_longlong(rc.obs);
+  v[17] = (unsigned long long)__double_as_longlong(rc.e);
+  v[18] = (unsigned long long)__double_as_longlong(rc.lz);
+  v[19] = (unsigned long long)__double_as_longlong(rc.q);
+  v[20] = pool_last;
+#pragma unroll
+  for (int k = 0; k < 21; ++k) __hip_atomic_store(&w[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // every store of the entry has left this wave before its flag is set
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&tl.eready[e], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+GDEV void early_load(const TailList& tl, uint64_t e, LoopState& s, RayConst& rc, uint32_t& pool_last) {
+  const unsigned long long* w = tl.est + e * EARLY_WORDS;
+  unsigned long long v[21];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) v[k] = __hip_atomic_load(&w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s.y[k] = __longlong_as_double((long long)v[k]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.c[k] = __longlong_as_double((long long)v[8 + k]);
+  s.h = __longlong_as_double((long long)v[11]);
+  s.h_cur = __longlong_as_double((long long)v[12]);
+  s.i = v[13];
+  s.idx = v[14];
+  s.nrec = (uint32_t)v[15];
+  s.retries = (int)((v[15] >> 32) & 0xffffu);
+  s.c_valid = ((v[15] >> 48) & 1u) != 0;
+  rc.obs = __longlong_as_double((long long)v[16]);
+  rc.e = __longlong_as_double((long long)v[17]);
+  rc.lz = __longlong_as_double((long long)v[18]);
+  rc.q = __longlong_as_double((long long)v[19]);
+  rc.pt = 0.0;
+  rc.pphi = 0.0;
+  pool_last = (uint32_t)v[20];
+}
 GDEV unsigned long long load_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A word another XCD writes while this kernel runs, read with an atomic (fetch-add of 0):
+// an atomic always sees the latest value, a load may be served from this XCD's L2.
+GDEV unsigned long long poll_agent(unsigned long long* p) {
+  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+GDEV unsigned int poll_agent(unsigned int* p) {
+  return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// `waves` integrate waves have exited (every early entry they reserved is written); the
+// last one of the launch tells early_tail_kernel (ctl[11]).  One lane per call.
+GDEV void integrate_wave_exit(const TailList& tl, unsigned waves) {
+  __threadfence();
+  const unsigned long long before = atomicAdd(&tl.ctl[10], (unsigned long long)waves);
+  if (before + waves == tl.int_waves) {
+    __threadfence();
+    __hip_atomic_store(&tl.ctl[11], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // One lane integrates one ray at a time: RKF45 attempts, and after every accepted
@@ -1488,13 +1558,17 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     const DevScene* __restrict__ Sp, WorkList wl, Workspace ws, unsigned long long* __restrict__ counter,
     unsigned long long* __restrict__ stats, TailList tl) {
   const DevScene& S = *Sp;
+  // items present: the capacity, or the count the adaptive pass decided on the device
+  const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
+  if (n_items == 0) {  // an empty chunk of a supersample pass
+    if (G == GRT_GEOM_KERR && tl.cap && tl.early_steps && threadIdx.x == 0) integrate_wave_exit(tl, blockDim.x / 64);
+    return;
+  }
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr uint64_t CHUNK = 64;
   const uint64_t n = ws.n;
-  // items present: the capacity, or the count the adaptive pass decided on the device
-  const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
   constexpr bool TAIL = (G == GRT_GEOM_KERR);
   const bool tail_on = TAIL && tl.cap != 0;
   constexpr int NKL = (((GRT_KLDS_GEOMS) >> G) & 1) ? GRT_KL_STAGES : 0;
@@ -1503,7 +1577,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
   bool started = false, ended = false;  // since the last live-count update (tail_on)
-  uint32_t poll = 0;
+  uint32_t poll = 0, epoll = 0;
   bool prio_high = false;  // GRT_LONG_PRIO: this wave's s_setprio level (wave-uniform)
   (void)prio_high;
   uint64_t idx = 0;      // output slot of the current ray
@@ -1603,19 +1677,78 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         started = ended = false;
         const long long d = (long long)__popcll(st_mask) - (long long)__popcll(en_mask);
         if (d != 0 && lane == 0) atomicAdd(&tl.ctl[0], (unsigned long long)d);
+        // early hand-off: rays past early_steps go to a waiting quad of early_tail_kernel
+        if (tl.early_steps && (++epoll & 15u) == 0u) {
+          const uint64_t cand = __ballot(active && i >= tl.early_steps);
+          if (cand) {
+            unsigned long long b = 0, k = 0;
+            if (lane == 0) {
+              const long long waiting = (long long)poll_agent(&tl.ctl[9]) - (long long)poll_agent(&tl.ctl[8]);
+              if (waiting > 0) {
+                k = min((unsigned long long)waiting, (unsigned long long)__popcll(cand));
+                b = atomicAdd(&tl.ctl[8], k);
+              }
+            }
+            k = __shfl(k, 0);
+            b = __shfl(b, 0);
+            const uint64_t r = __popcll(cand & lanemask_lt);
+            if (((cand >> lane) & 1ull) && r < k && b + r < tl.early_cap) {
+              LoopState s;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) s.y[q] = y[q];
+#pragma unroll
+              for (int q = 0; q < 3; ++q) s.c[q] = c[q];
+              s.h = h;
+              s.h_cur = h_cur;
+              s.i = i;
+              s.idx = idx;
+              s.nrec = nrec;
+              s.retries = retries;
+              s.c_valid = c_valid;
+              // the ray's last pool record (this lane wrote it): hit_append's next link
+              const uint32_t last = nrec > GRT_WS_SLOTS ? ws.pool->last[idx] : HIT_NIL;
+              early_save(tl, b + r, s, rc, last);
+              active = false;  // the lane takes new work; the ray is no longer live here
+              ended = true;
+            }
+          }
+        }
         // hand-off: queue drained (and nothing left in this wave's chunk), few rays left
         if ((chunk_next >= chunk_end || chunk_next >= n_items) && ((++poll & 15u) == 0u) &&
             load_agent(counter) >= n_items &&
             (long long)load_agent(&tl.ctl[0]) <= (long long)tl.threshold) {
           const uint64_t ev = __ballot(active);
           if (ev) {
-            unsigned long long b = 0;
+            unsigned long long b = 0, be = 0;
             if (lane == 0) {
               b = atomicAdd(&tl.ctl[1], (unsigned long long)__popcll(ev));
               if (b == 0) tl.ctl[5] = __builtin_amdgcn_s_memrealtime();
+              // early hand-off on: these rays join the early list too (tickets serve them)
+              if (tl.early_steps) be = atomicAdd(&tl.ctl[8], (unsigned long long)__popcll(ev));
             }
             b = __shfl(b, 0);
-            if (active) {
+            be = __shfl(be, 0);
+            if (active && tl.early_steps) {
+              const uint64_t e = be + __popcll(ev & lanemask_lt);
+              if (e < tl.early_cap) {
+                LoopState s;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s.y[k] = y[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) s.c[k] = c[k];
+                s.h = h;
+                s.h_cur = h_cur;
+                s.i = i;
+                s.idx = idx;
+                s.nrec = nrec;
+                s.retries = retries;
+                s.c_valid = c_valid;
+                const uint32_t last = nrec > GRT_WS_SLOTS ? ws.pool->last[idx] : HIT_NIL;
+                early_save(tl, e, s, rc, last);
+                active = false;
+                done = true;
+              }
+            } else if (active) {
               const uint64_t e = b + __popcll(ev & lanemask_lt);
               if (e < tl.cap) {
                 LoopState s;
@@ -1630,7 +1763,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
                 s.nrec = nrec;
                 s.retries = retries;
                 s.c_valid = c_valid;
-                tail_save(tl, e, s);
+                tail_save(tl.st, tl.cap, e, s);
                 active = false;
                 done = true;
               }
@@ -1726,9 +1859,46 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     atomicAdd(stats + 1, (unsigned long long)n_att);
     atomicAdd(stats + 2, (unsigned long long)n_rays);
   }
+  if constexpr (TAIL) {
+    if (tail_on && tl.early_steps) integrate_wave_exit(tl, 1);
+  }
 }
 
 // ============================================================= tail kernel =======
+// One attempt of a handed-off ray on the 4 lanes of its quad: the loop body of
+// integrate_kernel with the RHS split over the quad (rhs_ks_quad); lane 0 of the quad
+// writes.  Returns true when the ray has ended (its outputs are stored).
+template <int G, bool VOL>
+GDEV bool quad_attempt(const DevScene& S, const Workspace& ws, const RayConst& rc, LoopState& s, int sub,
+                       bool writer, uint64_t& n_acc, uint64_t& n_att) {
+  double yn[8];
+  const double err_sq = rkf_attempt<G, false, true>(S, rc, s.y, s.h_cur, yn, sub);
+  n_att++;
+  double h_next;
+  const int ctl = step_control(S, err_sq, s.h_cur, s.retries, h_next);
+  if (ctl != STEP_ACCEPTED) {
+    if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
+      if (writer) store_ray(ws, s.idx, s.y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)s.i);
+      return true;
+    }
+    return false;
+  }
+  s.h = h_next;
+  s.i++;
+  n_acc++;
+  window_pass<G, VOL>(S, ws, rc, s.idx, s.y, yn, s.c, s.c_valid, s.i, s.nrec, writer);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s.y[k] = yn[k];
+  const int stop = should_stop<G>(S, s.y, s.c, s.c_valid, s.i);
+  if (stop != GRT_STOP_NONE || s.i == S.max_steps - 1) {
+    if (writer) store_ray(ws, s.idx, s.y, stop, GRT_OK, s.nrec, (uint32_t)s.i);
+    return true;
+  }
+  s.retries = 0;
+  s.h_cur = rclamp(s.h, H_MIN, H_MAX);
+  return false;
+}
+
 // The rays integrate_kernel handed off (Kerr-Schild): the 4 lanes of a quad carry one
 // ray, splitting each RHS evaluation (rhs_ks_quad), and repeat the rest of the loop of
 // integrate_kernel in lockstep (identical values in all four lanes; lane 0 of the quad
@@ -1765,7 +1935,7 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
         if (e >= n_tail) {
           done = true;
         } else {
-          tail_load(tl, e, s);
+          tail_load(tl.st, tl.cap, e, s);
           rc.obs = ws.rc[0 * n + s.idx];
           rc.e = ws.rc[1 * n + s.idx];
           rc.lz = ws.rc[2 * n + s.idx];
@@ -1778,33 +1948,7 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
     }
     if (__ballot(!done) == 0) break;
     if (!active) continue;
-
-    double yn[8];
-    const double err_sq = rkf_attempt<G, false, true>(S, rc, s.y, s.h_cur, yn, sub);
-    n_att++;
-    double h_next;
-    const int ctl = step_control(S, err_sq, s.h_cur, s.retries, h_next);
-    if (ctl != STEP_ACCEPTED) {
-      if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
-        if (writer) store_ray(ws, s.idx, s.y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)s.i);
-        active = false;
-      }
-      continue;
-    }
-    s.h = h_next;
-    s.i++;
-    n_acc++;
-    window_pass<G, VOL>(S, ws, rc, s.idx, s.y, yn, s.c, s.c_valid, s.i, s.nrec, writer);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s.y[k] = yn[k];
-    const int stop = should_stop<G>(S, s.y, s.c, s.c_valid, s.i);
-    if (stop != GRT_STOP_NONE || s.i == S.max_steps - 1) {
-      if (writer) store_ray(ws, s.idx, s.y, stop, GRT_OK, s.nrec, (uint32_t)s.i);
-      active = false;
-      continue;
-    }
-    s.retries = 0;
-    s.h_cur = rclamp(s.h, H_MIN, H_MAX);
+    if (quad_attempt<G, VOL>(S, ws, rc, s, sub, writer, n_acc, n_att)) active = false;
   }
 
   if (lane == 0) atomicMax(&tl.ctl[6], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1817,6 +1961,99 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
   if (lane == 0) {
     atomicAdd(stats + 0, (unsigned long long)n_acc);
     atomicAdd(stats + 1, (unsigned long long)n_att);
+  }
+}
+
+// ======================================================= early tail kernel =======
+// Beside the integrate kernel, on its own CUs (api.hip: a CU-masked stream): the rays the
+// integrate kernel moves here once they pass tl.early_steps accepted steps, each on a
+// quad as in tail_kernel.  An idle quad takes a ticket (ctl[9]) and waits for that entry
+// of the early list; the integrate kernel hands a ray over only while a ticket is
+// unserved, so no ray waits here for a quad.  After the integrate kernel has ended
+// (ctl[11]) a ticket without an entry ends its quad.  Scheduling only: the quad runs the
+// same operations as a lane would (bit-identical, tests/test_tail.py).
+constexpr unsigned long long EARLY_WATCHDOG_TICKS = 360000000000ull;  // 1 h at 100 MHz: never in a real frame
+
+template <int G>
+__global__ void __launch_bounds__(256, GRT_TAIL_WAVES) early_tail_kernel(const DevScene* __restrict__ Sp,
+                                                                         Workspace ws, TailList tl,
+                                                                         unsigned long long* __restrict__ stats,
+                                                                         int instance) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before any lookup
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & 3;
+  const bool writer = sub == 0;
+  const uint64_t below_quad = (lane < 4) ? 0ull : (~0ull >> (64 - (lane & ~3)));
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+  bool active = false, done = false, waiting = false;
+  uint64_t ticket = 0;
+  LoopState s;
+  RayConst rc;
+  uint64_t n_acc = 0, n_att = 0;
+
+  while (true) {
+    const uint64_t takers = __ballot(!active && !done && !waiting && writer);
+    if (takers) {
+      unsigned long long b = 0;
+      if (lane == 0) b = atomicAdd(&tl.ctl[9], (unsigned long long)__popcll(takers));
+      b = __shfl(b, 0);
+      if (!active && !done && !waiting) {
+        ticket = b + __popcll(takers & below_quad);
+        waiting = true;
+      }
+    }
+    if (waiting) {
+      // the quad's lane 0 polls, with atomics: a plain or sc1 load of a line this XCD's
+      // L2 already holds would not see another XCD's store (measured: flags never seen)
+      bool got = false;
+      done = false;
+      if (writer) {
+        const bool in_list = ticket < tl.early_cap;
+        got = in_list && poll_agent(&tl.eready[ticket]) != 0u;
+        if (!got) {
+          if (poll_agent(&tl.ctl[11]) != 0ull) {  // the integrate kernel has ended: every entry is published
+            got = in_list && poll_agent(&tl.eready[ticket]) != 0u;
+            done = !got;
+          } else if (__builtin_amdgcn_s_memrealtime() - t0 > EARLY_WATCHDOG_TICKS) {
+            atomicMax(&tl.ctl[13], 1ull);  // reported as an error by the host
+            done = true;
+          }
+        }
+      }
+      // one decision per quad (its four lanes run the ray in lockstep)
+      got = __shfl((int)got, lane & ~3) != 0;
+      done = __shfl((int)done, lane & ~3) != 0;
+      waiting = !got && !done;
+      if (got) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        uint32_t last;
+        early_load(tl, ticket, s, rc, last);
+        if (writer && s.nrec > GRT_WS_SLOTS) ws.pool->last[s.idx] = last;  // before this CU appends after it
+        waiting = false;
+        active = true;
+      }
+    }
+    if (__ballot(!done) == 0) break;
+    if (!active) {
+      if (__ballot(active) == 0) __builtin_amdgcn_s_sleep(32);  // the whole wave waits for entries
+      continue;
+    }
+    if (quad_attempt<G, false>(S, ws, rc, s, sub, writer, n_acc, n_att)) active = false;
+  }
+
+  if (lane == 0) atomicMax(&tl.ctl[12], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (!writer) n_acc = n_att = 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    n_acc += __shfl_down(n_acc, off);
+    n_att += __shfl_down(n_att, off);
+  }
+  if (lane == 0) {
+    atomicAdd(stats + 0, (unsigned long long)n_acc);
+    atomicAdd(stats + 1, (unsigned long long)n_att);
+    atomicAdd(&tl.ctl[14 + instance], (unsigned long long)n_acc);  // grt_early_report
   }
 }
 
@@ -2328,9 +2565,12 @@ template <int G, int MODE>
 __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__ Sp, Workspace ws, Outputs out,
                                                     unsigned long long* __restrict__ stats) {
   const DevScene& S = *Sp;
-  glibc::tables_to_lds();  // whole block, before the early return
   const uint64_t n = ws.n;
   const uint64_t n_live = ws.n_live ? (uint64_t)min((unsigned long long)n, *ws.n_live) : n;
+  // a block past the live rays (the empty chunks of a supersample pass) has nothing to do;
+  // block 0 stays for the pool high-water mark below
+  if (blockIdx.x != 0 && (uint64_t)blockIdx.x * blockDim.x >= n_live) return;
+  glibc::tables_to_lds();  // whole block, before the early return
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if constexpr (MODE == 1) {
     const uint32_t mask = idx < n_live ? march_slots<G>(S, ws, idx) : 0u;
@@ -2458,10 +2698,40 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
 template <int G>
 static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
                            unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
-                           bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream) {
+                           bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream,
+                           const EarlySplit* es) {
   const unsigned nb = (unsigned)((ws.n + 255) / 256);
   TailList tl = tl_in;
   if (G != GRT_GEOM_KERR || tail_blocks <= 0) tl.cap = 0;
+  if (G != GRT_GEOM_KERR || vol || !tl.cap || !es) tl.early_steps = 0;
+  if constexpr (G == GRT_GEOM_KERR) {
+    if (tl.early_steps) {  // integrate beside early_tail_kernel, on disjoint CU sets
+      hipError_t e;
+      if ((e = hipEventRecord(es->fork, stream)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(es->s_int, es->fork, 0)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(es->s_early, es->fork, 0)) != hipSuccess) return e;
+      hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, es->s_int, d_scene, wl, ws,
+                         d_counter, d_stats, tl);
+      if ((e = hipGetLastError()) != hipSuccess) return e;  // nothing waits for an early kernel yet
+      hipLaunchKernelGGL((early_tail_kernel<G>), dim3(es->early_blocks), dim3(256), 0, es->s_early, d_scene, ws, tl,
+                         d_stats, 0);
+      const hipError_t le = hipGetLastError();  // without it no ticket is taken until the second one below
+      // the rest of the early list (the final hand-off's entries) on the integrate kernel's
+      // CUs once it has ended; the early kernel's quads take part of them too
+      hipLaunchKernelGGL((early_tail_kernel<G>), dim3(tail_blocks), dim3(256), 0, es->s_int, d_scene, ws, tl, d_stats,
+                         1);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      if ((e = hipEventRecord(es->int_done, es->s_int)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(stream, es->int_done, 0)) != hipSuccess) return e;
+      if (le == hipSuccess) {
+        if ((e = hipEventRecord(es->early_done, es->s_early)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(stream, es->early_done, 0)) != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL((shade_kernel<G, 0>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      return le;
+    }
+  }
   if (!vol) {
     hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
                        d_counter, d_stats, tl);
@@ -2498,24 +2768,25 @@ static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Wo
 
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
-                        int threads, bool vol, const TailList& tl, int tail_blocks, hipStream_t stream) {
+                        int threads, bool vol, const TailList& tl, int tail_blocks, hipStream_t stream,
+                        const EarlySplit* es) {
   if (ws.n == 0) return hipSuccess;
   switch (geometry) {
     case GRT_GEOM_EUCLIDEAN:
       return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
-                                          tail_blocks, stream);
+                                          tail_blocks, stream, nullptr);
     case GRT_GEOM_SCHWARZSCHILD:
       return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
-                                              tail_blocks, stream);
+                                              tail_blocks, stream, nullptr);
     case GRT_GEOM_KERR:
       return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl, tail_blocks,
-                                     stream);
+                                     stream, es);
     case GRT_GEOM_KERR_BL:
       return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
-                                        tail_blocks, stream);
+                                        tail_blocks, stream, nullptr);
     case GRT_GEOM_EUCLIDEAN_SPHERICAL:
       return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
-                                                    tl, tail_blocks, stream);
+                                                    tl, tail_blocks, stream, nullptr);
     default:
       return hipErrorInvalidValue;
   }

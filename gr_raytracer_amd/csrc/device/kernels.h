@@ -9,13 +9,24 @@ namespace grt {
 // integrate_kernel (persistent, lane refill) then shade_kernel, all on `stream`.  With
 // `vol` (the scene has VolumetricDiscs): integrate, job gathering, march_kernel and the
 // composite; the workspace then needs its volumetric arrays, ws.march zeroed.
-// `tl.cap` != 0 (Kerr-Schild without volumetric objects only): long rays are handed to
+// `tl.cap` != 0 (every Kerr-Schild trace, volumetric or not): long rays are handed to
 // tail_kernel (launched between integrate and shade on `stream`, `tail_blocks` blocks of
 // 256 threads); tl.ctl must be zeroed.
+// `es` (nullable; Kerr-Schild without volumetric objects, tl.early_steps != 0): the
+// early hand-off.  The integrate kernel runs on es->s_int and early_tail_kernel
+// (es->early_blocks blocks) on es->s_early, two CU-masked streams with disjoint CU sets,
+// both after `stream`'s earlier work (es->fork); `stream` waits for the integrate kernel
+// (es->int_done) before tail_kernel and for the early kernel (es->early_done) before
+// shade_kernel.  `blocks` is then the integrate grid, and tl.int_waves its waves.
+struct EarlySplit {
+  hipStream_t s_int, s_early;
+  hipEvent_t fork, int_done, early_done;
+  int early_blocks;
+};
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
                         int blocks, int threads, bool vol, const TailList& tl, int tail_blocks,
-                        hipStream_t stream);
+                        hipStream_t stream, const EarlySplit* es = nullptr);
 // Tail kernel's quad capacity per block (rays integrated at once).
 constexpr int TAIL_RAYS_PER_BLOCK = 256 / 4;
 

@@ -240,3 +240,39 @@ def test_failed_subsamples_are_reported(grt, oracle, gpu):
         finally:
             oracle.lib().oracle_set_libm_perturbation(0)
         assert moved.all(), diff
+
+
+def test_supersample_chunks_are_bit_identical(grt, gpu):
+    """The supersample pass runs its selected pixels in chunks of sub-rays, each chunk's
+    live count read on the device (grt_set_sub_chunk).  Forcing 7 pixels per chunk (many
+    chunks, the last one partly filled, most of the worst-case chunks empty) gives the
+    same frame, selection and failed sub-sample list as the default single chunk."""
+    import ctypes as C
+    import math
+
+    from gr_raytracer_amd import _lib as L
+
+    b = grt.SceneBuilder(1, radius=2.0, horizon_epsilon=1e-4)
+    b.integration(20000, 100.0, 0.01, 1e-7)
+    pos = grt.cartesian_to_spherical((0.0, -16.0, 0.0, 3.5))
+    vel = grt.stationary_velocity(1, 2.0, 0.0, pos)
+    b.camera(pos, vel, math.pi / 4, 48, 48, 0.0, -3.142, 0.0)
+    b.celestial(grt.Checker(0.0, 20.0, 20.0, (0, 255, 0), (0, 100, 0)))
+    b.add_disc(3.0, 12.0, grt.BlackBody(1.0), temperature=5000.0)  # BelowRISCO sub-rays
+    d = b.build()
+    sc = grt.Scene(C.pointer(d), keepalive=(d, b))
+    ad = grt.scene.default_adaptive()
+    ad.enabled, ad.samples_per_axis = 1, 4
+    one = sc.render_section_ex(adaptive=ad, log_events=True)
+    assert one.n_supersampled > 21 and one.n_supersampled % 7 != 0 and len(one.failed_subsamples) > 10
+    try:
+        L.check(L.lib().grt_set_sub_chunk(7 * 16), "grt_set_sub_chunk")
+        many = sc.render_section_ex(adaptive=ad, log_events=True)
+    finally:
+        L.check(L.lib().grt_set_sub_chunk(0), "grt_set_sub_chunk")
+    assert many.n_supersampled == one.n_supersampled
+    assert np.array_equal(many.xyza64.view(np.uint64), one.xyza64.view(np.uint64))
+    assert np.array_equal(many.ray_class, one.ray_class) and np.array_equal(many.status, one.status)
+    assert np.array_equal(many.failed_subsamples, one.failed_subsamples)
+    assert np.array_equal(many.subsample_events, one.subsample_events)
+    assert many.stats["accepted_steps"] == one.stats["accepted_steps"]

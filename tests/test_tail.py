@@ -55,6 +55,52 @@ def test_tail_hand_off_is_bit_identical(grt, gpu, rect):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rect", [(1816, 2792, 24, 24), (1536, 1536, 64, 1024)])
+def test_early_hand_off_is_bit_identical(grt, gpu, rect):
+    """The early hand-off (early_tail_kernel beside the integrate kernel on CU-masked
+    streams; the final hand-off's rays through the same early list) at C4's camera,
+    max_steps 1e5: every ray eligible from its first step with 8 early CUs, from 5000
+    steps with 32, and off, give the same colours, classes, statuses, stop reasons, step
+    counts and totals as integrating each ray on one lane."""
+    hs = host_scene(grt, "kerr.toml", c4_opts(grt, max_steps=100000))
+    sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
+    try:
+        _set_tail(grt, 0)
+        grt.scene.set_early_tail(0)
+        base, _ = _render(grt, sc, rect)
+        assert base.steps.max() > 50000
+        _set_tail(grt, -1)
+        other = (rect[0] + rect[2], rect[1] - rect[3], rect[2], rect[3])
+        for steps, cus in ((1, 8), (5000, 32), (0, 0)):
+            grt.scene.set_early_tail(steps, cus)
+            sc.render_pixels(*other)  # the workspace then holds other rays: nothing stale can pass
+            got, handed = _render(grt, sc, rect)
+            er = sc.early_report()
+            if steps:
+                assert er["cus"] == cus, er
+                assert er["handed_early"] > 0, (steps, er)
+                assert er["steps_beside"] > 0, (steps, er)  # the early kernel beside the integrate kernel worked
+            else:
+                assert er["cus"] == 0 or er["handed_early"] == 0
+            assert np.array_equal(got.xyza64, base.xyza64), (steps, cus)
+            assert np.array_equal(got.xyza, base.xyza), (steps, cus)
+            for f in ("ray_class", "status", "steps", "stop_reason", "hits"):
+                assert np.array_equal(getattr(got, f), getattr(base, f)), (steps, cus, f)
+            for k in ("accepted_steps", "attempts", "rays"):
+                assert got.stats[k] == base.stats[k], (steps, cus, k)
+    finally:
+        _set_tail(grt, -1)
+        grt.scene.set_early_tail(0)
+
+
+def test_set_early_tail_rejects_bad_arguments(grt):
+    lib = grt._lib.lib()
+    assert lib.grt_set_early_tail(-2, 0) != 0
+    assert lib.grt_set_early_tail(-1, -1) != 0
+    assert lib.grt_set_early_tail(-1, 0) == 0
+
+
+@pytest.mark.gpu
 def test_tail_hand_off_is_bit_identical_volumetric(grt, gpu):
     """kerr-volumetric-stony.toml (Kerr-Schild + VolumetricDisc) with C4's camera: the
     handed-off rays keep their volumetric window records (chord directions, frequency
@@ -79,3 +125,38 @@ def test_tail_hand_off_is_bit_identical_volumetric(grt, gpu):
                 assert got.stats[k] == base.stats[k], (mode, k)
     finally:
         _set_tail(grt, -1)
+
+
+@pytest.mark.gpu
+def test_c4_production_shard_matches_oracle(grt, oracle, gpu):
+    """configs[3]'s production path at full max-steps (1e6): a 1/64 cyclic row-band shard
+    of the 4096^2 kerr.toml frame (16-row bands, shard 0: it holds the rows through the
+    hole) through grt_render_shard with everything on automatic -- the probe-ordered
+    tile queue, exact-count claims and the long-ray hand-off to tail_kernel -- checked
+    against the oracle on ~540 pixels stratified over the shard plus its 16 longest rays
+    (the ones the hand-off carries), with check_parity's bar applied lazily
+    (raytracer.rs:195-244, kerr.rs:149-241)."""
+    from gr_raytracer_amd.distributed import shard_frame_rows
+    from test_gpu_frames import lazy_parity, oracle_pixels, stratified
+
+    hs = host_scene(grt, "kerr.toml", c4_opts(grt))
+    sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
+    _set_tail(grt, -1)
+    r = sc.render_shard(16, 0, 64, aux=True)
+    rep = sc.tail_report(capacity=1 << 16)
+    cols = sc.cols
+    frame_rows = shard_frame_rows(sc.rows, 16, 0, 64)
+    assert len(frame_rows) == 64 and r.steps.size == 64 * cols
+    assert rep["handed_off"] > 0  # the hand-off ran
+    assert r.steps.max() >= 500000  # the shard holds the long rays the hand-off exists for
+    lr, ci = stratified(64, cols, 23, 17)
+    k = lr * cols + ci
+    longest = np.argsort(-r.steps.astype(np.int64), kind="stable")[:16]
+    k = np.unique(np.concatenate([k, longest]))
+    assert np.isin(longest, rep["slot"]).any()  # some of them finished in tail_kernel
+    lr, ci = k // cols, k % cols
+    ri = frame_rows[lr]
+    got = {"xyza": r.xyza[k], "xyza64": r.xyza64[k], "ray_class": r.ray_class[k], "status": r.status[k],
+           "stop": r.stop_reason[k], "steps": r.steps[k]}
+    ref = oracle_pixels(oracle, hs.desc, cols, ri, ci)
+    lazy_parity(oracle, hs.desc, cols, ri, ci, got, ref)
