@@ -1860,7 +1860,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     atomicAdd(stats + 2, (unsigned long long)n_rays);
   }
   if constexpr (TAIL) {
-    if (tail_on && tl.early_steps) integrate_wave_exit(tl, 1);
+    if (tail_on && tl.early_steps && lane == 0) integrate_wave_exit(tl, 1);  // one lane per wave
   }
 }
 
