@@ -1589,7 +1589,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   int retries = 0;
   uint32_t nrec = 0;
   RayConst rc;
-  uint64_t n_acc = 0, n_att = 0, n_rays = 0;
+  // per-lane counters in 32 bits (one VGPR each): a lane integrates far fewer than 2^32
+  // steps in one launch (C4 whole frame: ~5e6 per lane)
+  uint32_t n_acc = 0, n_att = 0, n_rays = 0;
 
   while (true) {
     // ---------------- lane refill: ballot, one atomic per 64 items --------------
@@ -1848,16 +1850,17 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   }
 
   // per-wave reduction of the counters, one atomic per wave
+  uint64_t w_acc = n_acc, w_att = n_att, w_rays = n_rays;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    n_acc += __shfl_down(n_acc, off);
-    n_att += __shfl_down(n_att, off);
-    n_rays += __shfl_down(n_rays, off);
+    w_acc += __shfl_down(w_acc, off);
+    w_att += __shfl_down(w_att, off);
+    w_rays += __shfl_down(w_rays, off);
   }
   if (lane == 0) {
-    atomicAdd(stats + 0, (unsigned long long)n_acc);
-    atomicAdd(stats + 1, (unsigned long long)n_att);
-    atomicAdd(stats + 2, (unsigned long long)n_rays);
+    atomicAdd(stats + 0, (unsigned long long)w_acc);
+    atomicAdd(stats + 1, (unsigned long long)w_att);
+    atomicAdd(stats + 2, (unsigned long long)w_rays);
   }
   if constexpr (TAIL) {
     if (tail_on && tl.early_steps && lane == 0) integrate_wave_exit(tl, 1);  // one lane per wave

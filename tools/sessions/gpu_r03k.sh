@@ -1,10 +1,10 @@
 #!/bin/bash
-# r03j: early hand-off after the one-lane wave-exit fix: crop stats, tail tests,
+# r03k: early hand-off (wave-exit fix, 32-bit lane counters): crop stats, tail tests,
 # C4 1/8 shard 2 with the early hand-off off and at three settings
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
-OUT=gpurun_out/r03j
+OUT=gpurun_out/r03k
 mkdir -p "$OUT"
 timeout -k 10 120 python3 tools/early_debug.py > "$OUT/early_debug.jsonl" 2>&1 || { cat "$OUT/early_debug.jsonl" >&2; exit 1; }
 cat "$OUT/early_debug.jsonl" >&2
