@@ -70,7 +70,16 @@ namespace grt {
 #define GRT_SLOW GDEV
 #endif
 GRT_SLOW double ocml_pow(double x, double y) { return pow(x, y); }
-GRT_SLOW void ocml_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+// returned by value: a pointer into the caller's frame passed to an out-of-line call would
+// keep the caller's (sin, cos) in scratch memory at every rsincos site, fast path included
+struct SinCos {
+  double s, c;
+};
+GRT_SLOW SinCos ocml_sincos(double x) {
+  SinCos r;
+  sincos(x, &r.s, &r.c);
+  return r;
+}
 GRT_SLOW double ocml_sin(double x) { return sin(x); }
 GRT_SLOW double ocml_cos(double x) { return cos(x); }
 
@@ -84,7 +93,14 @@ GDEV double rpow(double x, double y) {
 // them into glibc's sincos (glibc_math.h); a lone sin() stays glibc's sin.  Both are
 // bit-exact for |x| < 105414350; OCML beyond (never reached by angles here).
 GDEV void rsincos(double x, double* s, double* c) {
-  if (!glibc::sincos_fast(x, s, c)) ocml_sincos(x, s, c);
+  double ss, cc;
+  if (!glibc::sincos_fast(x, &ss, &cc)) {
+    const SinCos r = ocml_sincos(x);
+    ss = r.s;
+    cc = r.c;
+  }
+  *s = ss;
+  *c = cc;
 }
 GDEV double rsin(double x) {
   double r;
@@ -1591,13 +1607,15 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   RayConst rc;
   // per-lane counters in 32 bits (one VGPR each): a lane integrates far fewer than 2^32
   // steps in one launch (C4 whole frame: ~5e6 per lane)
-  uint32_t n_acc = 0, n_att = 0, n_rays = 0;
+  uint32_t n_acc = 0, n_att = 0;
+  uint64_t w_rays = 0;  // rays started by this wave: counted in wave-uniform control flow (an SGPR)
 
   while (true) {
     // ---------------- lane refill: ballot, one atomic per 64 items --------------
     bool need = !active && !done;
     uint64_t need_mask = __ballot(need);
     if (need_mask) {
+      bool fresh = false;  // this lane started a ray in this refill
       uint64_t cnt = __popcll(need_mask);
       uint64_t remaining = chunk_end - chunk_next;
       uint64_t new_base = 0;
@@ -1656,7 +1674,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
             nrec = 0;
             active = true;
             started = true;
-            n_rays++;
+            fresh = true;
             if (S.max_steps <= 1) {  // `for i in 1..max_steps` never runs
               store_ray(ws, idx, y, GRT_STOP_NONE, GRT_OK, 0, 0);
               active = false;
@@ -1665,6 +1683,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
           }
         }
       }
+      w_rays += __popcll(__ballot(fresh));
       if (cnt > remaining) {
         chunk_next = new_base + (cnt - remaining);
         chunk_end = new_base + take;
@@ -1680,7 +1699,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         const long long d = (long long)__popcll(st_mask) - (long long)__popcll(en_mask);
         if (d != 0 && lane == 0) atomicAdd(&tl.ctl[0], (unsigned long long)d);
         // early hand-off: rays past early_steps go to a waiting quad of early_tail_kernel
-        if (tl.early_steps && (++epoll & 15u) == 0u) {
+        if (tl.early_steps && (++epoll & 63u) == 0u) {
           const uint64_t cand = __ballot(active && i >= tl.early_steps);
           if (cand) {
             unsigned long long b = 0, k = 0;
@@ -1850,12 +1869,11 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   }
 
   // per-wave reduction of the counters, one atomic per wave
-  uint64_t w_acc = n_acc, w_att = n_att, w_rays = n_rays;
+  uint64_t w_acc = n_acc, w_att = n_att;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     w_acc += __shfl_down(w_acc, off);
     w_att += __shfl_down(w_att, off);
-    w_rays += __shfl_down(w_rays, off);
   }
   if (lane == 0) {
     atomicAdd(stats + 0, (unsigned long long)w_acc);
@@ -2007,40 +2025,49 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) early_tail_kernel(const D
         waiting = true;
       }
     }
-    if (waiting) {
-      // the quad's lane 0 polls, with atomics: a plain or sc1 load of a line this XCD's
-      // L2 already holds would not see another XCD's store (measured: flags never seen)
-      bool got = false;
-      done = false;
-      if (writer) {
-        const bool in_list = ticket < tl.early_cap;
-        got = in_list && poll_agent(&tl.eready[ticket]) != 0u;
-        if (!got) {
-          if (poll_agent(&tl.ctl[11]) != 0ull) {  // the integrate kernel has ended: every entry is published
-            got = in_list && poll_agent(&tl.eready[ticket]) != 0u;
-            done = !got;
-          } else if (__builtin_amdgcn_s_memrealtime() - t0 > EARLY_WATCHDOG_TICKS) {
-            atomicMax(&tl.ctl[13], 1ull);  // reported as an error by the host
-            done = true;
+    if (__ballot(waiting)) {
+      // polls are atomics: a plain or sc1 load of a line this XCD's L2 already holds would
+      // not see another XCD's store (measured: flags never seen).  The integrate kernel's
+      // end (ctl[11]) is polled once per wave, before the quads' flags: once it is seen,
+      // every entry is published, so a flag still clear then stays clear.
+      unsigned long long ended = 0;
+      if (lane == 0) ended = poll_agent(&tl.ctl[11]);
+      ended = __shfl(ended, 0);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (waiting) {
+        bool got = false;
+        done = false;
+        if (writer) {
+          const bool in_list = ticket < tl.early_cap;
+          got = in_list && poll_agent(&tl.eready[ticket]) != 0u;
+          if (!got) {
+            if (ended != 0ull) {
+              done = true;
+            } else if (__builtin_amdgcn_s_memrealtime() - t0 > EARLY_WATCHDOG_TICKS) {
+              atomicMax(&tl.ctl[13], 1ull);  // reported as an error by the host
+              done = true;
+            }
           }
         }
-      }
-      // one decision per quad (its four lanes run the ray in lockstep)
-      got = __shfl((int)got, lane & ~3) != 0;
-      done = __shfl((int)done, lane & ~3) != 0;
-      waiting = !got && !done;
-      if (got) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        uint32_t last;
-        early_load(tl, ticket, s, rc, last);
-        if (writer && s.nrec > GRT_WS_SLOTS) ws.pool->last[s.idx] = last;  // before this CU appends after it
-        waiting = false;
-        active = true;
+        // one decision per quad (its four lanes run the ray in lockstep)
+        got = __shfl((int)got, lane & ~3) != 0;
+        done = __shfl((int)done, lane & ~3) != 0;
+        waiting = !got && !done;
+        if (got) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          uint32_t last;
+          early_load(tl, ticket, s, rc, last);
+          if (writer && s.nrec > GRT_WS_SLOTS) ws.pool->last[s.idx] = last;  // before this CU appends after it
+          waiting = false;
+          active = true;
+        }
       }
     }
     if (__ballot(!done) == 0) break;
     if (!active) {
-      if (__ballot(active) == 0) __builtin_amdgcn_s_sleep(32);  // the whole wave waits for entries
+      if (__ballot(active) == 0) {  // the whole wave waits for entries: ~13 us between polls
+        for (int z = 0; z < 4; ++z) __builtin_amdgcn_s_sleep(127);
+      }
       continue;
     }
     if (quad_attempt<G, false>(S, ws, rc, s, sub, writer, n_acc, n_att)) active = false;
