@@ -6,6 +6,10 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/r03o_c4full; mkdir -p $OUT
 T="python3 tools/prof_target.py c4full"
+# heartbeat: a pass runs ~5 minutes without output
+( while true; do sleep 50; date >> $OUT/heartbeat.txt; echo tick >&2; done ) &
+HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d $OUT/fetch -o run --pmc FETCH_SIZE -- $T > $OUT/fetch.log 2>&1 || exit 1
 echo fetch done >&2
 timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d $OUT/write -o run --pmc WRITE_SIZE -- $T > $OUT/write.log 2>&1 || exit 1
