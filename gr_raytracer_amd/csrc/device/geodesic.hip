@@ -1594,6 +1594,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   bool active = false, done = false;
   bool started = false, ended = false;  // since the last live-count update (tail_on)
   uint32_t poll = 0, epoll = 0;
+  bool q_drained = false;  // this wave has seen the tile queue drained (it stays drained)
   bool prio_high = false;  // GRT_LONG_PRIO: this wave's s_setprio level (wave-uniform)
   (void)prio_high;
   uint64_t idx = 0;      // output slot of the current ray
@@ -1734,9 +1735,12 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
             }
           }
         }
-        // hand-off: queue drained (and nothing left in this wave's chunk), few rays left
-        if ((chunk_next >= chunk_end || chunk_next >= n_items) && ((++poll & 15u) == 0u) &&
-            load_agent(counter) >= n_items &&
+        // hand-off: queue drained (and nothing left in this wave's chunk), few rays left.
+        // Kerr-Schild claims exactly what it starts, so its chunk is always used up: the
+        // drained test (an agent-scope load, served beyond this XCD's L2) runs every 256
+        // attempts until the wave has seen the queue drained, then the live count every 16
+        if ((chunk_next >= chunk_end || chunk_next >= n_items) && ((++poll & (q_drained ? 15u : 255u)) == 0u) &&
+            (q_drained || (q_drained = load_agent(counter) >= n_items)) &&
             (long long)load_agent(&tl.ctl[0]) <= (long long)tl.threshold) {
           const uint64_t ev = __ballot(active);
           if (ev) {
