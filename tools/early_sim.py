@@ -6,8 +6,9 @@ Each (T, k) pair: rays move to a free quad of the k early CUs once they pass T a
 steps (T = 0: no early hand-off).  Model: a lane runs LANE_US per step while the chip is
 full, a quad QUAD_US; the probe-ordered tile queue is rebuilt as tools/tail_replay.py
 does; the final hand-off moves every live ray to the whole chip's quads once the queue is
-drained and at most 64 rays per CU are live.  Calibrated on the measured shard without
-the early hand-off (drain 26.9 s, end 49.9 s, profiles/r03k)."""
+drained and at most 64 rays per CU are live.  Not calibrated: with LANE_US = 45 it
+matches the measured drain (27 s) but puts the final hand-off at ~37 s against the
+measured 45.5 s (profiles/r03k, r03m), so it cannot rank schedules."""
 import sys
 
 import numpy as np
