@@ -28,10 +28,7 @@ int g_blocks_per_cu = 0;
 int g_threads = 256;
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
 long long g_tail = -1;  // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
-long long g_early = 0;  // grt_set_early_tail: -1 auto, 0 off (default off until measured), > 0 accepted steps before a ray moves early
-int g_early_cus = 0;     // CUs of the early tail kernel (0: automatic)
 constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
-constexpr uint64_t EARLY_STEPS_AUTO = 100000;  // accepted steps before a ray may move early (automatic mode)
 
 
 int fail(int code, const std::string& msg) {
@@ -81,14 +78,6 @@ struct DeviceCopy {
   unsigned long long* d_tail_ctl = nullptr;  // 16 words (TailList::ctl)
   uint64_t tail_cap = 0;
   unsigned long long* tail_mem = nullptr;
-  // early hand-off: the early list (32-word entries + flags, grow-only), the two CU-masked
-  // streams (integrate / early tail kernel) and their events; split_cus = the early CU count
-  // the streams were made for (-1: CU masks unavailable on this device)
-  uint64_t early_cap = 0;
-  void* early_mem = nullptr;
-  int split_cus = 0;
-  hipStream_t s_int = nullptr, s_early = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_int = nullptr, ev_early = nullptr;
   // hit pool: window candidates past a ray's GRT_WS_SLOTS workspace slots, grow-only
   uint64_t pool_cap = 0;
   bool pool_vol = false;
@@ -568,84 +557,28 @@ int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList*
   return 0;
 }
 
-// The early list for n output slots: 32-word entries (two cache lines each) + a flag per
-// entry.  Grow-only.
-int early_list(DeviceCopy& dc, uint64_t n, grt::TailList* tl) {
-  const uint64_t entry_bytes = 32 * sizeof(unsigned long long);
-  if (n > dc.early_cap || !dc.early_mem) {
-    if (dc.early_mem) {
+#if GRT_RAY_TIMES
+// Diagnostic builds: the per-ray schedule record of the last trace ([6][n] words,
+// geodesic.hip), one process-wide buffer (single-device diagnostics).
+unsigned long long* g_rt = nullptr;
+uint64_t g_rt_cap = 0, g_rt_n = 0;
+int ray_times_reserve(uint64_t n, hipStream_t stream) {
+  if (n > g_rt_cap) {
+    if (g_rt) {
       (void)hipDeviceSynchronize();
-      (void)hipFree(dc.early_mem);
-      dc.early_mem = nullptr;
+      (void)hipFree(g_rt);
     }
-    dc.early_cap = 0;
-    const uint64_t cap = std::max<uint64_t>(n, 1 << 16);
-    HIP_TRY(hipMalloc(&dc.early_mem, cap * entry_bytes + cap * sizeof(unsigned int) + 256));
-    dc.early_cap = cap;
+    g_rt = nullptr;
+    g_rt_cap = 0;
+    HIP_TRY(hipMalloc(&g_rt, n * 6 * 8));
+    g_rt_cap = n;
   }
-  tl->est = (unsigned long long*)dc.early_mem;
-  tl->eready = (unsigned int*)((char*)dc.early_mem + dc.early_cap * entry_bytes);
-  tl->early_cap = n;
+  g_rt_n = n;
+  HIP_TRY(hipMemsetAsync(g_rt, 0, n * 6 * 8, stream));
+  HIP_TRY(grt::set_ray_times(g_rt));
   return 0;
 }
-
-// CU mask of `k` early CUs spread over the XCDs and shader engines whatever the order of
-// the mask's bits (XCD-major or XCD-interleaved): bit j * (cus / k) + j % 8.
-static void early_cu_mask(int cus, int k, bool early, std::vector<uint32_t>* mask) {
-  mask->assign((cus + 31) / 32, 0u);
-  std::vector<char> pick(cus, 0);
-  for (int j = 0; j < k; ++j) pick[(j * (cus / k) + j % 8) % cus] = 1;
-  for (int c = 0; c < cus; ++c)
-    if ((pick[c] != 0) == early) (*mask)[c / 32] |= 1u << (c % 32);
-}
-
-// Decide the early hand-off of one trace and make its streams: returns the early CU
-// count (0: not used) or a negative errno.  Kerr-Schild rectangle traces (frames and
-// row shards) without volumetric objects, when rays may run far past an escaping ray's
-// length (max_steps >= 2^18), with the long-ray hand-off on.
-int early_split(const grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, grt::TailList& tl, grt::EarlySplit* es) {
-  tl.early_steps = 0;
-  tl.est = nullptr;
-  tl.eready = nullptr;
-  tl.early_cap = 0;
-  tl.int_waves = 0;
-  if (g_early == 0 || !tl.cap || dc.vol || wl.pixel_index || wl.n_live || s->desc.geometry != GRT_GEOM_KERR)
-    return 0;
-  if (g_early < 0 && s->desc.max_steps < (1ull << 18)) return 0;
-  const int k = g_early_cus > 0 ? g_early_cus : std::max(8, dc.cus / 16);
-  if (k >= dc.cus || dc.split_cus < 0) return 0;
-  if (dc.split_cus != k) {
-    if (dc.s_int) (void)hipStreamDestroy(dc.s_int);
-    if (dc.s_early) (void)hipStreamDestroy(dc.s_early);
-    dc.s_int = dc.s_early = nullptr;
-    dc.split_cus = 0;
-    std::vector<uint32_t> m_int, m_early;
-    early_cu_mask(dc.cus, k, false, &m_int);
-    early_cu_mask(dc.cus, k, true, &m_early);
-    if (hipExtStreamCreateWithCUMask(&dc.s_int, (uint32_t)m_int.size(), m_int.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&dc.s_early, (uint32_t)m_early.size(), m_early.data()) != hipSuccess) {
-      (void)hipGetLastError();
-      if (dc.s_int) (void)hipStreamDestroy(dc.s_int);
-      dc.s_int = dc.s_early = nullptr;
-      dc.split_cus = -1;  // no CU masks here: every trace runs without the early hand-off
-      return 0;
-    }
-    if (!dc.ev_fork) {
-      HIP_TRY(hipEventCreateWithFlags(&dc.ev_fork, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&dc.ev_int, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&dc.ev_early, hipEventDisableTiming));
-    }
-    dc.split_cus = k;
-  }
-  tl.early_steps = g_early > 0 ? (uint64_t)g_early : EARLY_STEPS_AUTO;
-  es->s_int = dc.s_int;
-  es->s_early = dc.s_early;
-  es->fork = dc.ev_fork;
-  es->int_done = dc.ev_int;
-  es->early_done = dc.ev_early;
-  es->early_blocks = k * GRT_TAIL_WAVES;
-  return k;
-}
+#endif
 
 // Enqueue one trace over `wl` on `stream`; counters are zeroed first.
 int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, const grt::Outputs& o,
@@ -681,25 +614,16 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   }
   ws.pool = dc.d_pool;
   HIP_TRY(hipMemsetAsync(dc.pool_desc.count, 0, sizeof(unsigned long long), stream));
+#if GRT_RAY_TIMES
+  if ((rc = ray_times_reserve(n_out, stream))) return rc;
+#endif
   grt::TailList tl;
   int tail_blocks = 0;
   rc = tail_list(s, dc, blocks * (uint64_t)threads, &tl, &tail_blocks);
   if (rc) return rc;
   if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 16 * sizeof(unsigned long long), stream));
-  grt::EarlySplit es;
-  const int early_cus = early_split(s, dc, wl, tl, &es);
-  if (early_cus < 0) return early_cus;
-  if (early_cus > 0) {
-    // the integrate kernel runs on the other CUs
-    blocks = (int)std::min<uint64_t>(max_blocks, (uint64_t)(dc.cus - early_cus) * 2 *
-                                                     grt::integrate_waves(s->desc.geometry, dc.vol));
-    tl.int_waves = (uint64_t)blocks * (uint64_t)((threads + 63) / 64);
-    tail_blocks = (dc.cus - early_cus) * GRT_TAIL_WAVES;  // the second early kernel, on the integrate CUs
-    if ((rc = early_list(dc, n_out, &tl))) return rc;
-    HIP_TRY(hipMemsetAsync(tl.eready, 0, n_out * sizeof(unsigned int), stream));
-  }
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
-                            dc.vol, tl, tail_blocks, stream, early_cus > 0 ? &es : nullptr));
+                            dc.vol, tl, tail_blocks, stream));
   return stream_done(dc, stream);
 }
 
@@ -789,22 +713,11 @@ int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double t
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(v, dc.d_tail_ctl, sizeof(v), hipMemcpyDeviceToHost));
   *handed_off = v[1];
-  const bool split = v[8] != 0 || v[9] != 0;  // the last trace ran with the early hand-off
   if (timeline_s) {  // s_memrealtime ticks at 100 MHz
     auto since = [&](unsigned long long t) { return (t && v[3]) ? (double)(long long)(t - v[3]) * 1e-8 : 0.0; };
     timeline_s[0] = since(v[4]);
     timeline_s[1] = since(v[5]);
-    timeline_s[2] = since(split ? v[12] : v[6]);
-  }
-  if (split && capacity && dc.early_mem) {  // the handed-off rays are in the early list
-    const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(v[8], dc.early_cap), capacity);
-    std::vector<unsigned long long> ent(n * 32);
-    HIP_TRY(hipMemcpy(ent.data(), dc.early_mem, n * 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (uint64_t k = 0; k < n; ++k) {
-      if (slot) slot[k] = ent[k * 32 + 14];
-      if (step) step[k] = ent[k * 32 + 13];
-    }
-    return 0;
+    timeline_s[2] = since(v[6]);
   }
   const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(v[1], dc.tail_cap), capacity);
   if (n && dc.tail_mem) {
@@ -814,42 +727,21 @@ int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double t
   return 0;
 }
 
-int grt_set_early_tail(long long steps, int cus) {
-  if (steps < -1) return fail(-EINVAL, "early hand-off threshold must be -1 (auto), 0 (off) or a step count");
-  if (cus < 0 || cus > 4096) return fail(-EINVAL, "early tail CU count must be 0 (auto) or a CU count");
-  g_early = steps;
-  g_early_cus = cus;
-  return 0;
-}
-
-int grt_early_report(grt_scene* scene, int device, uint64_t* handed_early, uint64_t* handed_final,
-                     double* early_end_s, int* cus, uint64_t early_steps[2]) {
-  if (!scene || !handed_early) return fail(-EINVAL, "null argument");
-  *handed_early = 0;
-  if (handed_final) *handed_final = 0;
-  if (early_end_s) *early_end_s = 0.0;
-  if (cus) *cus = 0;
-  if (early_steps) early_steps[0] = early_steps[1] = 0;
-  if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
-    return 0;
+#if GRT_RAY_TIMES
+// Diagnostic builds only (not in grt_api.h): the last trace's per-ray schedule record,
+// [6][n] words (start, hand-off, end, hardware place, integrate / tail attempts), and
+// the integrate kernel's start (s_memrealtime) in *t0.
+int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n, uint64_t* t0) {
+  if (!scene || !out || !t0) return fail(-EINVAL, "null argument");
+  if (n != g_rt_n || !g_rt) return fail(-EINVAL, "ray count differs from the last trace");
   DeviceCopy& dc = *scene->devices[device];
-  std::lock_guard<std::mutex> lock(dc.mu);
   HIP_TRY(hipSetDevice(device));
-  unsigned long long v[16];
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(v, dc.d_tail_ctl, sizeof(v), hipMemcpyDeviceToHost));
-  if (v[13]) return fail(-EIO, "early tail kernel watchdog: the integrate kernel did not finish");
-  // [8] counts every early-list entry; [1] the final hand-off's share of them
-  *handed_early = v[8] >= v[1] ? v[8] - v[1] : 0;
-  if (handed_final) *handed_final = v[1];
-  if (early_end_s && v[12] && v[3]) *early_end_s = (double)(long long)(v[12] - v[3]) * 1e-8;
-  if (cus) *cus = dc.split_cus > 0 ? dc.split_cus : 0;
-  if (early_steps) {
-    early_steps[0] = v[14];
-    early_steps[1] = v[15];
-  }
+  HIP_TRY(hipMemcpy(out, g_rt, n * 6 * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(t0, dc.d_tail_ctl + 3, 8, hipMemcpyDeviceToHost));
   return 0;
 }
+#endif
 
 int grt_set_schedule(int mode) {
   if (mode < -1 || mode > 1) return fail(-EINVAL, "schedule mode must be -1 (auto), 0 or 1");
@@ -904,11 +796,6 @@ int grt_scene_destroy(grt_scene* s) {
     if (dc->ev0) (void)hipEventDestroy(dc->ev0);
     if (dc->ev1) (void)hipEventDestroy(dc->ev1);
     if (dc->ev_busy) (void)hipEventDestroy(dc->ev_busy);
-    for (hipEvent_t e : {dc->ev_fork, dc->ev_int, dc->ev_early})
-      if (e) (void)hipEventDestroy(e);
-    if (dc->s_int) (void)hipStreamDestroy(dc->s_int);
-    if (dc->s_early) (void)hipStreamDestroy(dc->s_early);
-    if (dc->early_mem) (void)hipFree(dc->early_mem);
     delete dc;
   }
   delete s;

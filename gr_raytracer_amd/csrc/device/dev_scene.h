@@ -215,32 +215,17 @@ constexpr int integrate_waves(int geometry, bool vol) {
 // quad (the three acceleration components of the Kerr-Schild RHS in parallel), one
 // wave per SIMD.  The split changes who computes a value, never its operations, so every
 // result is identical to integrating the ray on one lane (tests/test_tail.py).
-//
-// Early hand-off (early_steps != 0, rectangle traces): early_tail_kernel runs the same
-// quad-split loop BESIDE the integrate kernel, on a CU subset of its own (a CU-masked
-// stream; the integrate kernel gets the complement).  Its idle quads take tickets
-// (ctl[9]); a lane whose ray has passed `early_steps` accepted steps moves the ray to
-// the early list while a ticket is unserved (ctl[9] > ctl[8]), and its lane takes new
-// work.  So the longest rays run most of their steps at the quad-split speed (~7x a lane's
-// speed on a busy chip) instead of ending the frame alone.  After the integrate kernel
-// has ended (ctl[11]), the early kernel's quads serve the final hand-off list too.
+
 struct TailList {
   // [0] live rays (started - ended), [1] rays handed off, [2] tail claim cursor; timeline
   // (s_memrealtime, 100 MHz): [3] integrate start, [4] queue drained, [5] first hand-off,
-  // [6] tail kernel end.  Early hand-off: [8] early entries reserved, [9] early tickets
-  // taken, [10] integrate waves exited, [11] integrate done, [12] early kernel end,
-  // [13] early-kernel watchdog fired (an error: the integrate kernel never finished)
+  // [6] tail kernel end
   unsigned long long* ctl;  // 16 words
   uint64_t cap;             // entries of st (0: hand-off disabled)
   uint64_t threshold;       // hand off once the queue is drained and live <= threshold
   // [16][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,
   // nrec | retries << 32 | c_valid << 48
   unsigned long long* st;
-  uint64_t early_steps;     // 0: no early hand-off
-  uint64_t early_cap;       // entries of est: one per output slot (a ray moves early at most once)
-  unsigned long long* est;  // [16][early_cap], entries like st's
-  unsigned int* eready;     // [early_cap] 1 once entry e is written (zeroed per trace)
-  uint64_t int_waves;       // waves of the integrate launch (the last one to exit sets ctl[11])
 };
 
 struct Outputs {

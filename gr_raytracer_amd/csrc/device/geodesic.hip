@@ -58,6 +58,9 @@ namespace grt {
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
+#ifndef GRT_RAY_TIMES
+#define GRT_RAY_TIMES 0  // diagnostic builds only: per-ray schedule record (tools/c4_ray_times.py)
+#endif
 
 // The OCML fallbacks below run outside glibc's fast paths only (never for the angles and
 // controller ratios of a render): out of line, so their code stays out of the hot loops.
@@ -1341,9 +1344,29 @@ GDEV int step_control(const DevScene& S, double err_sq, double& h_cur, int& retr
 }
 
 // End of a ray: its final state goes to the workspace for the shade kernel.
+#if GRT_RAY_TIMES
+// Per-ray schedule record of a diagnostic build, [6][n] words at output slot idx: start,
+// hand-off and end (s_memrealtime, 100 MHz), the starting lane's hardware place
+// (XCC_ID << 32 | HW_ID), attempts in the integrate kernel, attempts in the tail kernel.
+__device__ unsigned long long* g_ray_times;
+GDEV void ray_time(uint64_t n, uint64_t idx, int k, unsigned long long v) {
+  if (g_ray_times) g_ray_times[(uint64_t)k * n + idx] = v;
+}
+GDEV unsigned long long hw_place() {
+  const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+  return ((unsigned long long)xcc << 32) | hw;
+}
+hipError_t set_ray_times(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_ray_times), &p, sizeof(p)); }
+#define RAY_TIME(n, idx, k, v) ray_time(n, idx, k, v)
+#else
+#define RAY_TIME(n, idx, k, v) ((void)0)
+#endif
+
 GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, int stop, int status, uint32_t nrec,
                     uint32_t steps) {
   const uint64_t n = ws.n;
+  RAY_TIME(n, idx, 2, __builtin_amdgcn_s_memrealtime());
 #pragma unroll
   for (int k = 0; k < 8; ++k) ws.y[k * n + idx] = y[k];
   ws.stop[idx] = (uint8_t)stop;
@@ -1489,81 +1512,9 @@ GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopSt
   s.retries = (int)((f >> 32) & 0xffffu);
   s.c_valid = ((f >> 48) & 1u) != 0;
 }
-// Early-list entry e: 32 words (256 B, two whole cache lines of its own) written once per
-// trace with write-through (sc1) stores and published by its eready flag; it carries the
-// per-ray constants and the ray's last hit-pool record too, so the early kernel (another
-// CU, often another XCD, in the same launch) reads nothing of the ray but this entry.
-constexpr uint64_t EARLY_WORDS = 32;
-GDEV void early_save(const TailList& tl, uint64_t e, const LoopState& s, const RayConst& rc, uint32_t pool_last) {
-  unsigned long long* w = tl.est + e * EARLY_WORDS;
-  unsigned long long v[21];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = (unsigned long long)__double_as_longlong(s.y[k]);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) v[8 + k] = (unsigned long long)__double_as_longlong(s.c[k]);
-  v[11] = (unsigned long long)__double_as_longlong(s.h);
-  v[12] = (unsigned long long)__double_as_longlong(s.h_cur);
-  v[13] = s.i;
-  v[14] = s.idx;
-  v[15] = (unsigned long long)s.nrec | ((unsigned long long)(uint32_t)s.retries << 32) |
-          ((unsigned long long)(s.c_valid ? 1 : 0) << 48);
-  v[16] = (unsigned long long)__double_as_longlong(rc.obs);
-  v[17] = (unsigned long long)__double_as_longlong(rc.e);
-  v[18] = (unsigned long long)__double_as_longlong(rc.lz);
-  v[19] = (unsigned long long)__double_as_longlong(rc.q);
-  v[20] = pool_last;
-#pragma unroll
-  for (int k = 0; k < 21; ++k) __hip_atomic_store(&w[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // every store of the entry has left this wave before its flag is set
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(&tl.eready[e], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-GDEV void early_load(const TailList& tl, uint64_t e, LoopState& s, RayConst& rc, uint32_t& pool_last) {
-  const unsigned long long* w = tl.est + e * EARLY_WORDS;
-  unsigned long long v[21];
-#pragma unroll
-  for (int k = 0; k < 21; ++k) v[k] = __hip_atomic_load(&w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s.y[k] = __longlong_as_double((long long)v[k]);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) s.c[k] = __longlong_as_double((long long)v[8 + k]);
-  s.h = __longlong_as_double((long long)v[11]);
-  s.h_cur = __longlong_as_double((long long)v[12]);
-  s.i = v[13];
-  s.idx = v[14];
-  s.nrec = (uint32_t)v[15];
-  s.retries = (int)((v[15] >> 32) & 0xffffu);
-  s.c_valid = ((v[15] >> 48) & 1u) != 0;
-  rc.obs = __longlong_as_double((long long)v[16]);
-  rc.e = __longlong_as_double((long long)v[17]);
-  rc.lz = __longlong_as_double((long long)v[18]);
-  rc.q = __longlong_as_double((long long)v[19]);
-  rc.pt = 0.0;
-  rc.pphi = 0.0;
-  pool_last = (uint32_t)v[20];
-}
 GDEV unsigned long long load_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// A word another XCD writes while this kernel runs, read with an atomic (fetch-add of 0):
-// an atomic always sees the latest value, a load may be served from this XCD's L2.
-GDEV unsigned long long poll_agent(unsigned long long* p) {
-  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-GDEV unsigned int poll_agent(unsigned int* p) {
-  return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// `waves` integrate waves have exited (every early entry they reserved is written); the
-// last one of the launch tells early_tail_kernel (ctl[11]).  One lane per call.
-GDEV void integrate_wave_exit(const TailList& tl, unsigned waves) {
-  __threadfence();
-  const unsigned long long before = atomicAdd(&tl.ctl[10], (unsigned long long)waves);
-  if (before + waves == tl.int_waves) {
-    __threadfence();
-    __hip_atomic_store(&tl.ctl[11], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // One lane integrates one ray at a time: RKF45 attempts, and after every accepted
 // step the chord test of window (previous step, step) against every object in config
 // order (objects.rs:81) and the stop test (window_pass, should_stop).
@@ -1576,10 +1527,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   const DevScene& S = *Sp;
   // items present: the capacity, or the count the adaptive pass decided on the device
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
-  if (n_items == 0) {  // an empty chunk of a supersample pass
-    if (G == GRT_GEOM_KERR && tl.cap && tl.early_steps && threadIdx.x == 0) integrate_wave_exit(tl, blockDim.x / 64);
-    return;
-  }
+  if (n_items == 0) return;  // an empty chunk of a supersample pass
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1593,7 +1541,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
   bool started = false, ended = false;  // since the last live-count update (tail_on)
-  uint32_t poll = 0, epoll = 0;
+  uint32_t poll = 0;
   bool q_drained = false;  // this wave has seen the tile queue drained (it stays drained)
   bool prio_high = false;  // GRT_LONG_PRIO: this wave's s_setprio level (wave-uniform)
   (void)prio_high;
@@ -1610,6 +1558,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   // steps in one launch (C4 whole frame: ~5e6 per lane)
   uint32_t n_acc = 0, n_att = 0;
   uint64_t w_rays = 0;  // rays started by this wave: counted in wave-uniform control flow (an SGPR)
+#if GRT_RAY_TIMES
+  uint32_t ray_att = 0;
+#endif
 
   while (true) {
     // ---------------- lane refill: ballot, one atomic per 64 items --------------
@@ -1676,6 +1627,11 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
             active = true;
             started = true;
             fresh = true;
+#if GRT_RAY_TIMES
+            ray_att = 0;
+            RAY_TIME(n, idx, 0, __builtin_amdgcn_s_memrealtime());
+            RAY_TIME(n, idx, 3, hw_place());
+#endif
             if (S.max_steps <= 1) {  // `for i in 1..max_steps` never runs
               store_ray(ws, idx, y, GRT_STOP_NONE, GRT_OK, 0, 0);
               active = false;
@@ -1699,42 +1655,6 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         started = ended = false;
         const long long d = (long long)__popcll(st_mask) - (long long)__popcll(en_mask);
         if (d != 0 && lane == 0) atomicAdd(&tl.ctl[0], (unsigned long long)d);
-        // early hand-off: rays past early_steps go to a waiting quad of early_tail_kernel
-        if (tl.early_steps && (++epoll & 63u) == 0u) {
-          const uint64_t cand = __ballot(active && i >= tl.early_steps);
-          if (cand) {
-            unsigned long long b = 0, k = 0;
-            if (lane == 0) {
-              const long long waiting = (long long)poll_agent(&tl.ctl[9]) - (long long)poll_agent(&tl.ctl[8]);
-              if (waiting > 0) {
-                k = min((unsigned long long)waiting, (unsigned long long)__popcll(cand));
-                b = atomicAdd(&tl.ctl[8], k);
-              }
-            }
-            k = __shfl(k, 0);
-            b = __shfl(b, 0);
-            const uint64_t r = __popcll(cand & lanemask_lt);
-            if (((cand >> lane) & 1ull) && r < k && b + r < tl.early_cap) {
-              LoopState s;
-#pragma unroll
-              for (int q = 0; q < 8; ++q) s.y[q] = y[q];
-#pragma unroll
-              for (int q = 0; q < 3; ++q) s.c[q] = c[q];
-              s.h = h;
-              s.h_cur = h_cur;
-              s.i = i;
-              s.idx = idx;
-              s.nrec = nrec;
-              s.retries = retries;
-              s.c_valid = c_valid;
-              // the ray's last pool record (this lane wrote it): hit_append's next link
-              const uint32_t last = nrec > GRT_WS_SLOTS ? ws.pool->last[idx] : HIT_NIL;
-              early_save(tl, b + r, s, rc, last);
-              active = false;  // the lane takes new work; the ray is no longer live here
-              ended = true;
-            }
-          }
-        }
         // hand-off: queue drained (and nothing left in this wave's chunk), few rays left.
         // Kerr-Schild claims exactly what it starts, so its chunk is always used up: the
         // drained test (an agent-scope load, served beyond this XCD's L2) runs every 256
@@ -1744,36 +1664,13 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
             (long long)load_agent(&tl.ctl[0]) <= (long long)tl.threshold) {
           const uint64_t ev = __ballot(active);
           if (ev) {
-            unsigned long long b = 0, be = 0;
+            unsigned long long b = 0;
             if (lane == 0) {
               b = atomicAdd(&tl.ctl[1], (unsigned long long)__popcll(ev));
               if (b == 0) tl.ctl[5] = __builtin_amdgcn_s_memrealtime();
-              // early hand-off on: these rays join the early list too (tickets serve them)
-              if (tl.early_steps) be = atomicAdd(&tl.ctl[8], (unsigned long long)__popcll(ev));
             }
             b = __shfl(b, 0);
-            be = __shfl(be, 0);
-            if (active && tl.early_steps) {
-              const uint64_t e = be + __popcll(ev & lanemask_lt);
-              if (e < tl.early_cap) {
-                LoopState s;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s.y[k] = y[k];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) s.c[k] = c[k];
-                s.h = h;
-                s.h_cur = h_cur;
-                s.i = i;
-                s.idx = idx;
-                s.nrec = nrec;
-                s.retries = retries;
-                s.c_valid = c_valid;
-                const uint32_t last = nrec > GRT_WS_SLOTS ? ws.pool->last[idx] : HIT_NIL;
-                early_save(tl, e, s, rc, last);
-                active = false;
-                done = true;
-              }
-            } else if (active) {
+            if (active) {
               const uint64_t e = b + __popcll(ev & lanemask_lt);
               if (e < tl.cap) {
                 LoopState s;
@@ -1789,6 +1686,8 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
                 s.retries = retries;
                 s.c_valid = c_valid;
                 tail_save(tl.st, tl.cap, e, s);
+                RAY_TIME(n, idx, 1, __builtin_amdgcn_s_memrealtime());
+                RAY_TIME(n, idx, 4, ray_att);
                 active = false;
                 done = true;
               }
@@ -1824,6 +1723,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
                    ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
                    : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
       n_att++;
+#if GRT_RAY_TIMES
+      ray_att++;
+#endif
       if constexpr (QUICK) {
         // every lane of the wave on the commonest accepted step (quick_step_ok): the
         // general path's updates in one straight-line block, then straight on to the next
@@ -1847,6 +1749,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     if (ctl != STEP_ACCEPTED) {
       if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
         store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
+        RAY_TIME(n, idx, 4, ray_att);
         active = false;
         ended = true;
       }
@@ -1864,6 +1767,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     int stop = should_stop<G>(S, y, c, c_valid, i);
     if (stop != GRT_STOP_NONE || i == S.max_steps - 1) {
       store_ray(ws, idx, y, stop, GRT_OK, nrec, (uint32_t)i);
+      RAY_TIME(n, idx, 4, ray_att);
       active = false;
       ended = true;
       continue;
@@ -1883,9 +1787,6 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     atomicAdd(stats + 0, (unsigned long long)w_acc);
     atomicAdd(stats + 1, (unsigned long long)w_att);
     atomicAdd(stats + 2, (unsigned long long)w_rays);
-  }
-  if constexpr (TAIL) {
-    if (tail_on && tl.early_steps && lane == 0) integrate_wave_exit(tl, 1);  // one lane per wave
   }
 }
 
@@ -1947,6 +1848,9 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
   LoopState s;
   RayConst rc;
   uint64_t n_acc = 0, n_att = 0;
+#if GRT_RAY_TIMES
+  uint64_t att0 = 0;
+#endif
 
   while (true) {
     const bool need = !active && !done;  // uniform within a quad
@@ -1968,12 +1872,20 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
           rc.pt = VOL ? ws.rc[4 * n + s.idx] : 0.0;
           rc.pphi = VOL ? ws.rc[5 * n + s.idx] : 0.0;
           active = true;
+#if GRT_RAY_TIMES
+          att0 = n_att;
+#endif
         }
       }
     }
     if (__ballot(!done) == 0) break;
     if (!active) continue;
-    if (quad_attempt<G, VOL>(S, ws, rc, s, sub, writer, n_acc, n_att)) active = false;
+    if (quad_attempt<G, VOL>(S, ws, rc, s, sub, writer, n_acc, n_att)) {
+      active = false;
+#if GRT_RAY_TIMES
+      if (writer) RAY_TIME(n, s.idx, 5, n_att - att0);
+#endif
+    }
   }
 
   if (lane == 0) atomicMax(&tl.ctl[6], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1986,108 +1898,6 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
   if (lane == 0) {
     atomicAdd(stats + 0, (unsigned long long)n_acc);
     atomicAdd(stats + 1, (unsigned long long)n_att);
-  }
-}
-
-// ======================================================= early tail kernel =======
-// Beside the integrate kernel, on its own CUs (api.hip: a CU-masked stream): the rays the
-// integrate kernel moves here once they pass tl.early_steps accepted steps, each on a
-// quad as in tail_kernel.  An idle quad takes a ticket (ctl[9]) and waits for that entry
-// of the early list; the integrate kernel hands a ray over only while a ticket is
-// unserved, so no ray waits here for a quad.  After the integrate kernel has ended
-// (ctl[11]) a ticket without an entry ends its quad.  Scheduling only: the quad runs the
-// same operations as a lane would (bit-identical, tests/test_tail.py).
-constexpr unsigned long long EARLY_WATCHDOG_TICKS = 360000000000ull;  // 1 h at 100 MHz: never in a real frame
-
-template <int G>
-__global__ void __launch_bounds__(256, GRT_TAIL_WAVES) early_tail_kernel(const DevScene* __restrict__ Sp,
-                                                                         Workspace ws, TailList tl,
-                                                                         unsigned long long* __restrict__ stats,
-                                                                         int instance) {
-  const DevScene& S = *Sp;
-  glibc::tables_to_lds();  // whole block, before any lookup
-  const int lane = threadIdx.x & 63;
-  const int sub = lane & 3;
-  const bool writer = sub == 0;
-  const uint64_t below_quad = (lane < 4) ? 0ull : (~0ull >> (64 - (lane & ~3)));
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-
-  bool active = false, done = false, waiting = false;
-  uint64_t ticket = 0;
-  LoopState s;
-  RayConst rc;
-  uint64_t n_acc = 0, n_att = 0;
-
-  while (true) {
-    const uint64_t takers = __ballot(!active && !done && !waiting && writer);
-    if (takers) {
-      unsigned long long b = 0;
-      if (lane == 0) b = atomicAdd(&tl.ctl[9], (unsigned long long)__popcll(takers));
-      b = __shfl(b, 0);
-      if (!active && !done && !waiting) {
-        ticket = b + __popcll(takers & below_quad);
-        waiting = true;
-      }
-    }
-    if (__ballot(waiting)) {
-      // polls are atomics: a plain or sc1 load of a line this XCD's L2 already holds would
-      // not see another XCD's store (measured: flags never seen).  The integrate kernel's
-      // end (ctl[11]) is polled once per wave, before the quads' flags: once it is seen,
-      // every entry is published, so a flag still clear then stays clear.
-      unsigned long long ended = 0;
-      if (lane == 0) ended = poll_agent(&tl.ctl[11]);
-      ended = __shfl(ended, 0);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (waiting) {
-        bool got = false;
-        done = false;
-        if (writer) {
-          const bool in_list = ticket < tl.early_cap;
-          got = in_list && poll_agent(&tl.eready[ticket]) != 0u;
-          if (!got) {
-            if (ended != 0ull) {
-              done = true;
-            } else if (__builtin_amdgcn_s_memrealtime() - t0 > EARLY_WATCHDOG_TICKS) {
-              atomicMax(&tl.ctl[13], 1ull);  // reported as an error by the host
-              done = true;
-            }
-          }
-        }
-        // one decision per quad (its four lanes run the ray in lockstep)
-        got = __shfl((int)got, lane & ~3) != 0;
-        done = __shfl((int)done, lane & ~3) != 0;
-        waiting = !got && !done;
-        if (got) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          uint32_t last;
-          early_load(tl, ticket, s, rc, last);
-          if (writer && s.nrec > GRT_WS_SLOTS) ws.pool->last[s.idx] = last;  // before this CU appends after it
-          waiting = false;
-          active = true;
-        }
-      }
-    }
-    if (__ballot(!done) == 0) break;
-    if (!active) {
-      if (__ballot(active) == 0) {  // the whole wave waits for entries: ~13 us between polls
-        for (int z = 0; z < 4; ++z) __builtin_amdgcn_s_sleep(127);
-      }
-      continue;
-    }
-    if (quad_attempt<G, false>(S, ws, rc, s, sub, writer, n_acc, n_att)) active = false;
-  }
-
-  if (lane == 0) atomicMax(&tl.ctl[12], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  if (!writer) n_acc = n_att = 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    n_acc += __shfl_down(n_acc, off);
-    n_att += __shfl_down(n_att, off);
-  }
-  if (lane == 0) {
-    atomicAdd(stats + 0, (unsigned long long)n_acc);
-    atomicAdd(stats + 1, (unsigned long long)n_att);
-    atomicAdd(&tl.ctl[14 + instance], (unsigned long long)n_acc);  // grt_early_report
   }
 }
 
@@ -2732,40 +2542,10 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
 template <int G>
 static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
                            unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
-                           bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream,
-                           const EarlySplit* es) {
+                           bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream) {
   const unsigned nb = (unsigned)((ws.n + 255) / 256);
   TailList tl = tl_in;
   if (G != GRT_GEOM_KERR || tail_blocks <= 0) tl.cap = 0;
-  if (G != GRT_GEOM_KERR || vol || !tl.cap || !es) tl.early_steps = 0;
-  if constexpr (G == GRT_GEOM_KERR) {
-    if (tl.early_steps) {  // integrate beside early_tail_kernel, on disjoint CU sets
-      hipError_t e;
-      if ((e = hipEventRecord(es->fork, stream)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(es->s_int, es->fork, 0)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(es->s_early, es->fork, 0)) != hipSuccess) return e;
-      hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, es->s_int, d_scene, wl, ws,
-                         d_counter, d_stats, tl);
-      if ((e = hipGetLastError()) != hipSuccess) return e;  // nothing waits for an early kernel yet
-      hipLaunchKernelGGL((early_tail_kernel<G>), dim3(es->early_blocks), dim3(256), 0, es->s_early, d_scene, ws, tl,
-                         d_stats, 0);
-      const hipError_t le = hipGetLastError();  // without it no ticket is taken until the second one below
-      // the rest of the early list (the final hand-off's entries) on the integrate kernel's
-      // CUs once it has ended; the early kernel's quads take part of them too
-      hipLaunchKernelGGL((early_tail_kernel<G>), dim3(tail_blocks), dim3(256), 0, es->s_int, d_scene, ws, tl, d_stats,
-                         1);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      if ((e = hipEventRecord(es->int_done, es->s_int)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(stream, es->int_done, 0)) != hipSuccess) return e;
-      if (le == hipSuccess) {
-        if ((e = hipEventRecord(es->early_done, es->s_early)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(stream, es->early_done, 0)) != hipSuccess) return e;
-      }
-      hipLaunchKernelGGL((shade_kernel<G, 0>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      return le;
-    }
-  }
   if (!vol) {
     hipLaunchKernelGGL((integrate_kernel<G, false>), dim3(blocks), dim3(threads), 0, stream, d_scene, wl, ws,
                        d_counter, d_stats, tl);
@@ -2802,25 +2582,24 @@ static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Wo
 
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats, int blocks,
-                        int threads, bool vol, const TailList& tl, int tail_blocks, hipStream_t stream,
-                        const EarlySplit* es) {
+                        int threads, bool vol, const TailList& tl, int tail_blocks, hipStream_t stream) {
   if (ws.n == 0) return hipSuccess;
   switch (geometry) {
     case GRT_GEOM_EUCLIDEAN:
       return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
-                                          tail_blocks, stream, nullptr);
+                                          tail_blocks, stream);
     case GRT_GEOM_SCHWARZSCHILD:
       return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
-                                              tail_blocks, stream, nullptr);
+                                              tail_blocks, stream);
     case GRT_GEOM_KERR:
       return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl, tail_blocks,
-                                     stream, es);
+                                     stream);
     case GRT_GEOM_KERR_BL:
       return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
-                                        tail_blocks, stream, nullptr);
+                                        tail_blocks, stream);
     case GRT_GEOM_EUCLIDEAN_SPHERICAL:
       return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
-                                                    tl, tail_blocks, stream, nullptr);
+                                                    tl, tail_blocks, stream);
     default:
       return hipErrorInvalidValue;
   }

@@ -12,21 +12,13 @@ namespace grt {
 // `tl.cap` != 0 (every Kerr-Schild trace, volumetric or not): long rays are handed to
 // tail_kernel (launched between integrate and shade on `stream`, `tail_blocks` blocks of
 // 256 threads); tl.ctl must be zeroed.
-// `es` (nullable; Kerr-Schild without volumetric objects, tl.early_steps != 0): the
-// early hand-off.  The integrate kernel runs on es->s_int and early_tail_kernel
-// (es->early_blocks blocks) on es->s_early, two CU-masked streams with disjoint CU sets,
-// both after `stream`'s earlier work (es->fork); `stream` waits for the integrate kernel
-// (es->int_done) before tail_kernel and for the early kernel (es->early_done) before
-// shade_kernel.  `blocks` is then the integrate grid, and tl.int_waves its waves.
-struct EarlySplit {
-  hipStream_t s_int, s_early;
-  hipEvent_t fork, int_done, early_done;
-  int early_blocks;
-};
 hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
                         const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
                         int blocks, int threads, bool vol, const TailList& tl, int tail_blocks,
-                        hipStream_t stream, const EarlySplit* es = nullptr);
+                        hipStream_t stream);
+// Diagnostic builds (-DGRT_RAY_TIMES=1): the per-ray schedule record ([6][n] words, see
+// geodesic.hip), or NULL.
+hipError_t set_ray_times(unsigned long long* p);
 // Tail kernel's quad capacity per block (rays integrated at once).
 constexpr int TAIL_RAYS_PER_BLOCK = 256 / 4;
 

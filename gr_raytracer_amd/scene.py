@@ -343,34 +343,15 @@ class Scene:
         step = np.zeros(capacity, np.uint64)
         L.check(L.lib().grt_tail_report(self._s, device, C.byref(n), tl, L.ptr(slot, C.c_uint64),
                                         L.ptr(step, C.c_uint64), capacity), "grt_tail_report")
-        er = self.early_report(device)
-        # with the early hand-off the slots list every ray of the early list (early + final)
-        k = min(n.value + er["handed_early"] if er["cus"] else n.value, capacity)
+        k = min(n.value, capacity)
         return {"handed_off": n.value, "drained_s": tl[0], "handoff_s": tl[1], "tail_end_s": tl[2],
-                "slot": slot[:k], "step": step[:k], **er}
-
-    def early_report(self, device: int = 0) -> dict:
-        """The last Kerr-Schild trace's early hand-off (grt_early_report): rays moved to the
-        early tail kernel, rays of the final hand-off, the tail kernels' end (s since the
-        integrate kernel started) and the early CU count (0: not used)."""
-        e, f, t, k = C.c_uint64(), C.c_uint64(), C.c_double(), C.c_int()
-        st = (C.c_uint64 * 2)()
-        L.check(L.lib().grt_early_report(self._s, device, C.byref(e), C.byref(f), C.byref(t), C.byref(k), st),
-                "grt_early_report")
-        return {"handed_early": e.value, "handed_final": f.value, "early_end_s": t.value, "cus": k.value,
-                "steps_beside": st[0], "steps_after": st[1]}
+                "slot": slot[:k], "step": step[:k]}
 
 
 def set_tail(threshold: int = -1) -> None:
     """Long-ray hand-off of Kerr-Schild traces (grt_set_tail): -1 auto, 0 off, > 0 the
     live-ray threshold.  Scheduling only; results are identical in every mode."""
     L.check(L.lib().grt_set_tail(int(threshold)), "grt_set_tail")
-
-
-def set_early_tail(steps: int = -1, cus: int = 0) -> None:
-    """Early hand-off of Kerr-Schild frames / shards (grt_set_early_tail): steps -1 auto,
-    0 off, > 0 the accepted steps before a ray may move; cus 0 auto.  Scheduling only."""
-    L.check(L.lib().grt_set_early_tail(int(steps), int(cus)), "grt_set_early_tail")
 
 
 # --------------------------------------------------------- programmatic scenes ----

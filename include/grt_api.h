@@ -595,23 +595,6 @@ int grt_set_schedule(int mode);
  * = the rays the tail kernel integrates at once, 64 per CU); 0 = off; > 0 = explicit
  * threshold.  Scheduling only: every pixel's result is identical in all modes. */
 int grt_set_tail(long long threshold);
-/* Early hand-off of Kerr-Schild frames and row shards (with the hand-off above on): a
- * tail kernel on `cus` CUs of its own runs beside the integrate kernel (two CU-masked
- * streams), and a ray that has passed `steps` accepted steps moves to it whenever one of
- * its quads waits for work, so the frame's longest rays run most of their steps at the
- * quad-split speed instead of ending the frame alone.  steps: -1 = automatic (default:
- * on when max_steps >= 2^18, 1e5 steps), 0 = off, > 0 = explicit; cus: 0 = automatic
- * (max(8, CUs / 16)).  Without CU masks on the device the trace runs without it.
- * Scheduling only: every pixel's result is identical in all modes. */
-int grt_set_early_tail(long long steps, int cus);
-/* The last Kerr-Schild trace's early hand-off on `device` (synchronises the device):
- * rays moved early, rays of the final hand-off (which the early list then also carries),
- * the tail kernels' end in seconds since the integrate kernel started, the early CU
- * count (0: not used), and the accepted steps integrated by the early tail kernel beside
- * the integrate kernel [0] and by the one after it [1].  Any pointer but handed_early
- * nullable; -EIO if the early kernel's watchdog fired (the trace is then incomplete). */
-int grt_early_report(grt_scene* scene, int device, uint64_t* handed_early, uint64_t* handed_final,
-                     double* early_end_s, int* cus, uint64_t early_steps[2]);
 /* Rays the last Kerr-Schild trace on `device` handed to the tail kernel (synchronises the
  * device; 0 before the first trace).  A diagnostic of the scheduling above. */
 int grt_tail_handoffs(grt_scene* scene, int device, uint64_t* handed_off);

@@ -55,55 +55,6 @@ def test_tail_hand_off_is_bit_identical(grt, gpu, rect):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rect", [(1816, 2792, 24, 24), (1536, 1536, 64, 1024)])
-def test_early_hand_off_is_bit_identical(grt, gpu, rect):
-    """The early hand-off (early_tail_kernel beside the integrate kernel on CU-masked
-    streams; the final hand-off's rays through the same early list) at C4's camera,
-    max_steps 1e5: every ray eligible from its first step with 8 early CUs, from 5000
-    steps with 32, and off, give the same colours, classes, statuses, stop reasons, step
-    counts and totals as integrating each ray on one lane."""
-    hs = host_scene(grt, "kerr.toml", c4_opts(grt, max_steps=100000))
-    sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
-    try:
-        _set_tail(grt, 0)
-        grt.scene.set_early_tail(0)
-        base, _ = _render(grt, sc, rect)
-        assert base.steps.max() > 50000
-        _set_tail(grt, -1)
-        other = (rect[0] + rect[2], rect[1] - rect[3], rect[2], rect[3])
-        for steps, cus in ((1, 8), (5000, 32), (0, 0)):
-            grt.scene.set_early_tail(steps, cus)
-            sc.render_pixels(*other)  # the workspace then holds other rays: nothing stale can pass
-            got, handed = _render(grt, sc, rect)
-            er = sc.early_report()
-            if steps:
-                assert er["cus"] == cus, er
-                # a small crop drains the queue at once: its final hand-off may take every ray
-                # before 5000 steps, and those entries are served from the same early list
-                assert er["handed_early"] > 0 if steps == 1 else er["handed_early"] + er["handed_final"] > 0, er
-                assert er["steps_beside"] > 0, (steps, er)  # the early kernel beside the integrate kernel worked
-                assert er["steps_beside"] + er["steps_after"] <= base.stats["accepted_steps"], er
-            else:
-                assert er["cus"] == 0 or er["handed_early"] == 0
-            assert np.array_equal(got.xyza64, base.xyza64), (steps, cus)
-            assert np.array_equal(got.xyza, base.xyza), (steps, cus)
-            for f in ("ray_class", "status", "steps", "stop_reason", "hits"):
-                assert np.array_equal(getattr(got, f), getattr(base, f)), (steps, cus, f)
-            for k in ("accepted_steps", "attempts", "rays"):
-                assert got.stats[k] == base.stats[k], (steps, cus, k)
-    finally:
-        _set_tail(grt, -1)
-        grt.scene.set_early_tail(0)
-
-
-def test_set_early_tail_rejects_bad_arguments(grt):
-    lib = grt._lib.lib()
-    assert lib.grt_set_early_tail(-2, 0) != 0
-    assert lib.grt_set_early_tail(-1, -1) != 0
-    assert lib.grt_set_early_tail(-1, 0) == 0
-
-
-@pytest.mark.gpu
 def test_tail_hand_off_is_bit_identical_volumetric(grt, gpu):
     """kerr-volumetric-stony.toml (Kerr-Schild + VolumetricDisc) with C4's camera: the
     handed-off rays keep their volumetric window records (chord directions, frequency

@@ -19,9 +19,6 @@ if "GRT_SCHEDULE" in os.environ:  # -1 auto, 0 row-major tiles, 1 probe-ordered
     L.check(L.lib().grt_set_schedule(int(os.environ["GRT_SCHEDULE"])))
 if "GRT_TAIL" in os.environ:  # -1 auto, 0 off, > 0 hand-off threshold
     L.check(L.lib().grt_set_tail(int(os.environ["GRT_TAIL"])))
-if "GRT_EARLY" in os.environ:  # "steps,cus": early hand-off (-1 auto, 0 off)
-    es, ec = (int(x) for x in os.environ["GRT_EARLY"].split(","))
-    g.scene.set_early_tail(es, ec)
 import hashlib  # noqa: E402
 n_shards = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 shards = [int(x) for x in sys.argv[2:]] or [0, n_shards // 2]
@@ -41,5 +38,4 @@ for s in shards:
                       "steps_per_s": st["accepted_steps"] / (st["kernel_ms"] * 1e-3),
                       "overflows": st["hit_overflows"], "schedule": os.environ.get("GRT_SCHEDULE", "auto"),
                       "tail": os.environ.get("GRT_TAIL", "auto"), "handoffs": sc.tail_handoffs(), "tail_timeline": tail,
-                      "early": os.environ.get("GRT_EARLY", "auto"), "early_report": sc.early_report(),
                       "md5": hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12]}), flush=True)
