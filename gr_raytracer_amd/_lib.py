@@ -161,6 +161,7 @@ def lib() -> C.CDLL:
         "grt_default_adaptive_config": (None, [C.POINTER(AdaptiveConfig)]),
         "grt_host_scene_load": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(GlobalOpts), C.POINTER(vp)]),
         "grt_host_scene_desc": (C.POINTER(SceneDesc), [vp]),
+        "grt_host_scene_log": (C.c_char_p, [vp]),
         "grt_host_geometry_load": (C.c_int, [C.c_char_p, C.POINTER(GlobalOpts), C.POINTER(vp)]),
         "grt_host_scene_adaptive": (None, [vp, C.POINTER(AdaptiveConfig)]),
         "grt_host_scene_destroy": (C.c_int, [vp]),
@@ -192,6 +193,7 @@ def lib() -> C.CDLL:
                                          C.POINTER(C.c_uint8)]),
         "grt_set_launch_config": (C.c_int, [C.c_int, C.c_int]),
         "grt_set_schedule": (C.c_int, [C.c_int]),
+        "grt_set_two_ended": (C.c_int, [C.c_int]),
         "grt_set_tail": (C.c_int, [C.c_longlong]),
         "grt_health_pixels": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.POINTER(Health), _pd]),
@@ -246,11 +248,11 @@ def lib() -> C.CDLL:
 
 EXPORTED_SYMBOLS = [
     "grt_last_error", "grt_device_count", "grt_default_global_opts", "grt_default_adaptive_config",
-    "grt_host_scene_load", "grt_host_geometry_load", "grt_host_scene_desc", "grt_host_scene_adaptive", "grt_host_scene_destroy",
+    "grt_host_scene_load", "grt_host_geometry_load", "grt_host_scene_desc", "grt_host_scene_log", "grt_host_scene_adaptive", "grt_host_scene_destroy",
     "grt_camera_build", "grt_stationary_velocity", "grt_zamo_velocity", "grt_cartesian_to_spherical",
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",
     "grt_blackbody_xyz", "grt_srgb_to_xyza", "grt_perlin_permutation", "grt_volumetric_frame", "grt_xyz_to_srgb8", "grt_xyz_to_srgb", "grt_blackbody_spectrum", "grt_linear_max", "grt_tonemap", "grt_scene_create", "grt_scene_destroy",
-    "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config", "grt_set_schedule", "grt_set_tail", "grt_tail_handoffs", "grt_health_pixels", "grt_tail_report",
+    "grt_render_pixels", "grt_render_pixels_async", "grt_render_section", "grt_set_launch_config", "grt_set_schedule", "grt_set_two_ended", "grt_set_tail", "grt_tail_handoffs", "grt_health_pixels", "grt_tail_report",
     "grt_shard_row_count", "grt_shard_frame_row", "grt_render_shard", "grt_render_shard_async", "grt_hit_pool_reserve", "grt_set_hit_pool_min", "grt_set_sub_chunk",
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",
     "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_adaptive_min_luminance_device", "grt_supersample_shard",

@@ -17,6 +17,7 @@
 // Extra (not in the reference): --device N selects the GPU, --resource-root DIR
 // resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer.
 #include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -130,6 +131,50 @@ static void log_ray_event(unsigned row, unsigned col, int stop, uint32_t accepte
                  "with %llu steps.\n", row, col, len);
 }
 
+// Rust's Debug form of an f64 ({:?}): Display's shortest digits, with ".0" on integral
+// values and exponential notation outside 1e-4 <= |v| < 1e16 (core::fmt::float).
+static std::string rust_debug_f64(double v) {
+  if (std::isnan(v) || std::isinf(v)) return grt_host::rust_display_f64(v);
+  const double a = std::fabs(v);
+  if (a != 0.0 && (a < 1e-4 || a >= 1e16)) {
+    char buf[64];
+    auto res = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);  // shortest digits
+    std::string sci(buf, res.ptr);
+    const size_t e = sci.find('e');
+    return sci.substr(0, e) + "e" + std::to_string(std::atoi(sci.c_str() + e + 1));
+  }
+  std::string d = grt_host::rust_display_f64(v);
+  if (d.find('.') == std::string::npos) d += ".0";
+  return d;
+}
+
+// CoordinateSystem's Debug form for the geometry (geometry/*.rs coordinate_system, point.rs:11)
+static std::string coordinate_system_debug(const grt_scene_desc* d) {
+  switch (d->geometry) {
+    case GRT_GEOM_SCHWARZSCHILD:
+    case GRT_GEOM_EUCLIDEAN_SPHERICAL: return "Spherical";
+    case GRT_GEOM_KERR_BL: return "BoyerLindquist { a: " + rust_debug_f64(d->a) + " }";
+    default: return "Cartesian";  // Euclidean, Kerr (Kerr-Schild)
+  }
+}
+
+// A Duration's Debug form with two decimals ({:.2?}, core::time: the largest unit of s /
+// ms / us / ns with a non-zero integer part; the dropped digits round half up).
+static std::string rust_duration_2(double secs) {
+  const unsigned long long ns = (unsigned long long)std::llround(secs * 1e9);
+  unsigned long long div;
+  const char* unit;
+  if (ns >= 1000000000ull) { div = 1000000000ull; unit = "s"; }
+  else if (ns >= 1000000ull) { div = 1000000ull; unit = "ms"; }
+  else if (ns >= 1000ull) { div = 1000ull; unit = "\u00b5s"; }
+  else { div = 1ull; unit = "ns"; }
+  if (div == 1) return std::to_string(ns) + ".00" + unit;
+  const unsigned long long hundredths = (ns * 100 + div / 2) / div;
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), "%llu.%02llu%s", hundredths / 100, hundredths % 100, unit);
+  return buf;
+}
+
 static const char* stop_name(int s) {  // integrator.rs StopReason, as logged by the reference
   switch (s) {
     case GRT_STOP_HORIZON: return "Some(HorizonReached)";
@@ -164,12 +209,12 @@ static int trace_and_save(grt_scene* scene, int device, const grt_scene_desc* d,
     std::fprintf(stderr, "Error: %s\n", status == GRT_ERR_MAX_STEPS_REACHED ? "Max steps reached" : "integration failed");
     return 1;
   }
-  std::fprintf(stderr, "Stop reason: %s\n", stop_name(stop));
+  std::fprintf(stderr, "[grt] INFO Stop reason: %s\n", stop_name(stop));
   if (grt_write_trajectory_csv(filename.c_str(), d->geometry, d->a, steps.data(), n < cap ? n : cap)) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
-  std::fprintf(stderr, "Saved integrated ray to %s\n", filename.c_str());
+  std::fprintf(stderr, "[grt] INFO Saved integrated ray to %s\n", filename.c_str());
   return 0;
 }
 
@@ -347,6 +392,21 @@ int main(int argc, char** argv) {
     return 1;
   }
   const grt_scene_desc* d = grt_host_scene_desc(hs);
+  auto elapsed = [&]() {  // main.rs:175-176
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    std::fprintf(stderr, "[grt] INFO Elapsed time: %s\n", rust_duration_2(secs).c_str());
+  };
+  if (action == "render")  // main.rs:100-103
+    std::fprintf(stderr, "[grt] INFO Using coordinate system: %s\n", coordinate_system_debug(d).c_str());
+  {  // the scene setup's info lines (KerrTemperatureComputer::new, temperature.rs:55-102)
+    const std::string log = grt_host_scene_log(hs);
+    for (size_t p = 0; p < log.size();) {
+      size_t q = log.find('\n', p);
+      if (q == std::string::npos) q = log.size();
+      std::fprintf(stderr, "[grt] INFO %s\n", log.substr(p, q - p).c_str());
+      p = q + 1;
+    }
+  }
   if (action != "render") {
     int rc;
     if (action == "render-ray") {  // Raytracer::integrate_ray_at_point (raytracer.rs:499-507)
@@ -370,6 +430,7 @@ int main(int argc, char** argv) {
     }
     grt_scene_destroy(scene);
     grt_host_scene_destroy(hs);
+    if (rc == 0) elapsed();
     return rc;
   }
   uint32_t r0 = from_row < 0 ? 0 : (uint32_t)from_row, c0 = from_col < 0 ? 0 : (uint32_t)from_col;
@@ -396,6 +457,14 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> stop((size_t)w * h);
   std::vector<uint32_t> steps((size_t)w * h);
   const bool supersampled = ac.enabled || maskp;
+  const bool hdr = filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".hdr") == 0;
+  if (hdr) {  // raytracer.rs:468-469, :481-483
+    std::fprintf(stderr, "[grt] INFO Creating HDR image\n");
+  } else {
+    std::fprintf(stderr, "[grt] INFO Creating non-HDR image\n");
+    std::fprintf(stderr, "[grt] INFO Tone mapping method: %s\n",
+                 opts.tone_mapping == GRT_TONE_GLOBAL_LINEAR ? "GlobalLinear" : "Reinhard");
+  }
   if (supersampled)  // raytracer.rs:264-267
     std::fprintf(stderr, "[grt] INFO Rendering section from (%u, %u) to (%u, %u) with supersampling\n", r0, c0, r1,
                  c1);
@@ -444,7 +513,7 @@ int main(int argc, char** argv) {
                  (unsigned long long)st.march_noise_samples, (unsigned long long)st.march_emit_samples);
   std::string err;
   bool ok;
-  if (filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".hdr") == 0) {
+  if (hdr) {
     std::vector<float> rgb((size_t)w * h * 3);
     for (size_t i = 0; i < (size_t)w * h; ++i)
       for (int k = 0; k < 3; ++k) rgb[3 * i + k] = (float)xyza[4 * i + k];
@@ -472,7 +541,7 @@ int main(int argc, char** argv) {
   }
   grt_scene_destroy(scene);
   grt_host_scene_destroy(hs);
-  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-  std::fprintf(stderr, "saved image to %s\nElapsed time: %.3f s\n", filename.c_str(), secs);
+  std::fprintf(stderr, "[grt] INFO saved image to %s\n", filename.c_str());  // raytracer.rs:494
+  elapsed();
   return 0;
 }

@@ -27,6 +27,7 @@ namespace {
 int g_blocks_per_cu = 0;
 int g_threads = 256;
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
+int g_two_ended = 1;  // grt_set_two_ended: probe-ordered traces take the queue from both ends
 long long g_tail = -1;  // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
 constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
 
@@ -588,6 +589,8 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   if (schedule_wanted(s, wl)) {
     int rc0 = enqueue_tile_order(s, dc, wl, stream, &wl.tile_order);
     if (rc0) return rc0;
+    // longest tiles to the priority wave of each SIMD, shortest to the others (WorkList)
+    wl.two_ended = (g_two_ended != 0 && wl.n_items < (1ull << 31)) ? 1u : 0u;
   }
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
   if (dc.vol) HIP_TRY(hipMemsetAsync(dc.d_march, 0, 2 * sizeof(unsigned long long), stream));  // jobs, cursor
@@ -599,7 +602,9 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   if ((uint64_t)blocks > max_blocks) blocks = (int)std::max<uint64_t>(1, max_blocks);
   uint64_t n_out = wl.pixel_index ? wl.n_items : (uint64_t)wl.rows * wl.cols;
   grt::Workspace ws;
-  int rc = ensure_pool(dc, n_out / 2);
+  // the pool starts at its minimum (grt_set_hit_pool_min) and only grows from a trace's
+  // measured need: the synchronous calls' re-trace of flagged pixels, grt_hit_pool_reserve
+  int rc = ensure_pool(dc, 0);
   if (rc) return rc;
   rc = ensure_workspace(dc, n_out, &ws);
   if (rc) return rc;
@@ -743,6 +748,12 @@ int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n,
 }
 #endif
 
+int grt_set_two_ended(int on) {
+  if (on != 0 && on != 1) return fail(-EINVAL, "two-ended queue: 0 or 1");
+  g_two_ended = on;
+  return 0;
+}
+
 int grt_set_schedule(int mode) {
   if (mode < -1 || mode > 1) return fail(-EINVAL, "schedule mode must be -1 (auto), 0 or 1");
   g_schedule = mode;
@@ -819,55 +830,159 @@ static int pool_check(DeviceCopy& dc, bool* again) {
   return 0;
 }
 
-// Trace `wl` (n output slots) into device scratch, wait, copy to the host arrays.
-static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, uint64_t n, float* xyza_out,
-                       uint8_t* class_out, uint8_t* status_out, const grt_aux_out* aux, grt_stats* stats) {
-  int rc;
-  DeviceCopy* dc = dc_;
-  DevBuf b_xyza, b_cls, b_status, b_x64, b_steps, b_stop, b_hits;
-  if ((rc = b_xyza.alloc(n * 16)) || (rc = b_cls.alloc(n)) || (rc = b_status.alloc(n))) return rc;
-  bool want64 = aux && aux->xyza64, want_steps = aux && aux->steps, want_stop = aux && aux->stop_reason;
-  bool want_hits = aux && aux->hits;
-  if (want64 && (rc = b_x64.alloc(n * 32))) return rc;
-  if (want_steps && (rc = b_steps.alloc(n * 4))) return rc;
-  if (want_stop && (rc = b_stop.alloc(n))) return rc;
-  if (want_hits && (rc = b_hits.alloc(n * 4))) return rc;
-  grt::Outputs o{(float*)b_xyza.p, (uint8_t*)b_cls.p, (uint8_t*)b_status.p, (double*)b_x64.p,
-                 (uint32_t*)b_steps.p, (uint8_t*)b_stop.p, (uint32_t*)b_hits.p};
-  hipStream_t st = nullptr;
-  for (bool again = true; again;) {
-    HIP_TRY(hipMemsetAsync(dc->d_stats, 0, 4 * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(dc->d_march, 0, 8 * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(dc->d_counter + 6, 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipEventRecord(dc->ev0, st));
-    if ((rc = enqueue_trace(s, *dc, wl, o, dc->d_stats, st))) return rc;
-    HIP_TRY(hipEventRecord(dc->ev1, st));
-    HIP_TRY(hipEventSynchronize(dc->ev1));
-    if ((rc = pool_check(*dc, &again))) return rc;
+// Device outputs of one synchronous trace of n slots (the aux ones when asked for).
+struct HostTrace {
+  DevBuf xyza, cls, status, x64, steps, stop, hits;
+  grt::Outputs o{};
+  int alloc(uint64_t n, const grt_aux_out* aux) {
+    int rc;
+    if ((rc = xyza.alloc(n * 16)) || (rc = cls.alloc(n)) || (rc = status.alloc(n))) return rc;
+    if (aux && aux->xyza64 && (rc = x64.alloc(n * 32))) return rc;
+    if (aux && aux->steps && (rc = steps.alloc(n * 4))) return rc;
+    if (aux && aux->stop_reason && (rc = stop.alloc(n))) return rc;
+    if (aux && aux->hits && (rc = hits.alloc(n * 4))) return rc;
+    o = grt::Outputs{(float*)xyza.p, (uint8_t*)cls.p, (uint8_t*)status.p, (double*)x64.p, (uint32_t*)steps.p,
+                     (uint8_t*)stop.p, (uint32_t*)hits.p};
+    return 0;
   }
-  HIP_TRY(hipMemcpy(xyza_out, b_xyza.p, n * 16, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(class_out, b_cls.p, n, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(status_out, b_status.p, n, hipMemcpyDeviceToHost));
-  if (want64) HIP_TRY(hipMemcpy(aux->xyza64, b_x64.p, n * 32, hipMemcpyDeviceToHost));
-  if (want_steps) HIP_TRY(hipMemcpy(aux->steps, b_steps.p, n * 4, hipMemcpyDeviceToHost));
-  if (want_stop) HIP_TRY(hipMemcpy(aux->stop_reason, b_stop.p, n, hipMemcpyDeviceToHost));
-  if (want_hits) HIP_TRY(hipMemcpy(aux->hits, b_hits.p, n * 4, hipMemcpyDeviceToHost));
+};
+
+// One trace of `wl` on the null stream, waited for.  Adds its counters to acc ([0..3]
+// accepted, attempts, rays, overflows; [4..7] march jobs, samples, noise, emitting
+// samples) and its event time to *ms; *need = hit-pool records it asked for.
+static int trace_sync(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, const grt::Outputs& o,
+                      unsigned long long acc[8], float* ms, unsigned long long* need) {
+  hipStream_t st = nullptr;
+  HIP_TRY(hipMemsetAsync(dc.d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc.d_march, 0, 8 * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(dc.d_counter + 6, 0, sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(dc.ev0, st));
+  if (int rc = enqueue_trace(s, dc, wl, o, dc.d_stats, st)) return rc;
+  HIP_TRY(hipEventRecord(dc.ev1, st));
+  HIP_TRY(hipEventSynchronize(dc.ev1));
+  unsigned long long h[4], m[8];
+  HIP_TRY(hipMemcpy(h, dc.d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(m, dc.d_march, sizeof(m), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(need, dc.d_counter + 6, sizeof(*need), hipMemcpyDeviceToHost));
+  float t = 0;
+  HIP_TRY(hipEventElapsedTime(&t, dc.ev0, dc.ev1));
+  for (int k = 0; k < 4; ++k) acc[k] += h[k];
+  acc[4] += m[3];
+  acc[5] += m[2];
+  acc[6] += m[4];
+  acc[7] += m[5];
+  *ms += t;
+  return 0;
+}
+
+// Trace `wl` (n output slots) into device scratch, wait, copy to the host arrays.  When the
+// hit pool was too small (the trace asked for more records than it had), only the pixels
+// that lost candidates (GRT_FLAG_HIT_OVERFLOW) are traced again, as a pixel list at their
+// centres (get_ray_for_offset at (0.5, 0.5) is get_ray_for, camera.rs:338-363), with the
+// pool grown once that subset alone does not fit; their outputs replace the flagged ones.
+// `offs` (host, nullable): the offsets list wl was built from.  The stats count the work
+// done, the re-traced rays included.
+static int run_to_host(grt_scene* s, DeviceCopy* dc_, const grt::WorkList& wl, uint64_t n, const grt_offsets* offs,
+                       float* xyza_out, uint8_t* class_out, uint8_t* status_out, const grt_aux_out* aux,
+                       grt_stats* stats) {
+  int rc;
+  DeviceCopy& dc = *dc_;
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float ms = 0;
+  unsigned long long need = 0;
+  {
+    HostTrace T;
+    if ((rc = T.alloc(n, aux)) || (rc = trace_sync(s, dc, wl, T.o, acc, &ms, &need))) return rc;
+    HIP_TRY(hipMemcpy(xyza_out, T.xyza.p, n * 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(class_out, T.cls.p, n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(status_out, T.status.p, n, hipMemcpyDeviceToHost));
+    if (T.o.xyza64) HIP_TRY(hipMemcpy(aux->xyza64, T.x64.p, n * 32, hipMemcpyDeviceToHost));
+    if (T.o.steps) HIP_TRY(hipMemcpy(aux->steps, T.steps.p, n * 4, hipMemcpyDeviceToHost));
+    if (T.o.stop) HIP_TRY(hipMemcpy(aux->stop_reason, T.stop.p, n, hipMemcpyDeviceToHost));
+    if (T.o.hits) HIP_TRY(hipMemcpy(aux->hits, T.hits.p, n * 4, hipMemcpyDeviceToHost));
+  }
+  // the flagged pixels, traced again until none is left (a round either fits or grows the
+  // pool to its own subset's need, which the next round's subset cannot exceed)
+  for (int round = 0; need > dc.pool_cap && round < 8; ++round) {
+    std::vector<uint64_t> lost;
+    for (uint64_t k = 0; k < n; ++k)
+      if (status_out[k] & GRT_FLAG_HIT_OVERFLOW) lost.push_back(k);
+    if (lost.empty()) break;
+    if (round > 0) {
+      if (dc.pool_cap >= POOL_MAX) break;  // cannot grow: the pixels stay flagged
+      if ((rc = ensure_pool(dc, need + need / 4))) return rc;
+    }
+    const uint64_t m = lost.size();
+    std::vector<uint32_t> pix(m);
+    std::vector<double> dx(m, 0.5), dy(m, 0.5);
+    grt::WorkList wo;
+    std::memset(&wo, 0, sizeof(wo));
+    wo.col0 = wl.col0;
+    wo.cols = wl.cols;
+    wo.n_items = m;
+    if (offs) {  // an offsets trace: the same (pixel, dx, dy) items
+      wo.row0 = wl.row0;
+      wo.rows = wl.rows;
+      for (uint64_t j = 0; j < m; ++j) {
+        pix[j] = offs->pixel_index[lost[j]];
+        dx[j] = offs->dx[lost[j]];
+        dy[j] = offs->dy[lost[j]];
+      }
+    } else if (wl.n_shards > 1) {  // a row-band shard: frame rows of the local ones
+      wo.row0 = 0;
+      wo.rows = (uint32_t)s->desc.camera.rows;
+      for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t lr = (uint32_t)(lost[j] / wl.cols), c = (uint32_t)(lost[j] % wl.cols);
+        pix[j] = grt::shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, lr) * wl.cols + c;
+      }
+    } else {
+      wo.row0 = wl.row0;
+      wo.rows = wl.rows;
+      for (uint64_t j = 0; j < m; ++j) pix[j] = (uint32_t)lost[j];
+    }
+    DevBuf b_pix, b_dx, b_dy;
+    if ((rc = b_pix.alloc(m * 4)) || (rc = b_dx.alloc(m * 8)) || (rc = b_dy.alloc(m * 8))) return rc;
+    HIP_TRY(hipMemcpy(b_pix.p, pix.data(), m * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b_dx.p, dx.data(), m * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b_dy.p, dy.data(), m * 8, hipMemcpyHostToDevice));
+    wo.pixel_index = (const uint32_t*)b_pix.p;
+    wo.dx = (const double*)b_dx.p;
+    wo.dy = (const double*)b_dy.p;
+    HostTrace T;
+    acc[3] = 0;  // the overflows of the last round are the ones left
+    if ((rc = T.alloc(m, aux)) || (rc = trace_sync(s, dc, wo, T.o, acc, &ms, &need))) return rc;
+    std::vector<float> x(m * 4);
+    std::vector<uint8_t> c(m), st(m), sp(T.o.stop ? m : 0);
+    std::vector<double> x64(T.o.xyza64 ? m * 4 : 0);
+    std::vector<uint32_t> ns(T.o.steps ? m : 0), nh(T.o.hits ? m : 0);
+    HIP_TRY(hipMemcpy(x.data(), T.xyza.p, m * 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c.data(), T.cls.p, m, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(st.data(), T.status.p, m, hipMemcpyDeviceToHost));
+    if (T.o.xyza64) HIP_TRY(hipMemcpy(x64.data(), T.x64.p, m * 32, hipMemcpyDeviceToHost));
+    if (T.o.steps) HIP_TRY(hipMemcpy(ns.data(), T.steps.p, m * 4, hipMemcpyDeviceToHost));
+    if (T.o.stop) HIP_TRY(hipMemcpy(sp.data(), T.stop.p, m, hipMemcpyDeviceToHost));
+    if (T.o.hits) HIP_TRY(hipMemcpy(nh.data(), T.hits.p, m * 4, hipMemcpyDeviceToHost));
+    for (uint64_t j = 0; j < m; ++j) {
+      const uint64_t k = lost[j];
+      std::memcpy(xyza_out + 4 * k, &x[4 * j], 16);
+      class_out[k] = c[j];
+      status_out[k] = st[j];
+      if (T.o.xyza64) std::memcpy(aux->xyza64 + 4 * k, &x64[4 * j], 32);
+      if (T.o.steps) aux->steps[k] = ns[j];
+      if (T.o.stop) aux->stop_reason[k] = sp[j];
+      if (T.o.hits) aux->hits[k] = nh[j];
+    }
+  }
   if (stats) {
-    unsigned long long h[4];
-    HIP_TRY(hipMemcpy(h, dc->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, dc->ev0, dc->ev1));
-    stats->accepted_steps = h[0];
-    stats->attempts = h[1];
-    stats->rays = h[2];
-    stats->hit_overflows = h[3];
+    stats->accepted_steps = acc[0];
+    stats->attempts = acc[1];
+    stats->rays = acc[2];
+    stats->hit_overflows = acc[3];
     stats->kernel_ms = ms;
-    unsigned long long m[8];
-    HIP_TRY(hipMemcpy(m, dc->d_march, sizeof(m), hipMemcpyDeviceToHost));
-    stats->march_jobs = m[3];
-    stats->march_samples = m[2];
-    stats->march_noise_samples = m[4];
-    stats->march_emit_samples = m[5];
+    stats->march_jobs = acc[4];
+    stats->march_samples = acc[5];
+    stats->march_noise_samples = acc[6];
+    stats->march_emit_samples = acc[7];
   }
   return 0;
 }
@@ -927,7 +1042,7 @@ int grt_render_pixels(grt_scene* s, int device, uint32_t row0, uint32_t col0, ui
   } else {
     wl = rect_worklist(row0, col0, rows, cols);
   }
-  return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
+  return run_to_host(s, dc, wl, n, offsets, xyza_out, class_out, status_out, aux, stats);
 }
 
 // Shared body of grt_trace_pixels / grt_trace_rays: a, b are (row, col) or (pos, mom).
@@ -1408,7 +1523,7 @@ int grt_render_shard(grt_scene* s, int device, const grt_row_shard* sh, float* x
   if ((rc = ensure_device(s, device, &dc))) return rc;
   std::lock_guard<std::mutex> lk(dc->mu);
   HIP_TRY(hipSetDevice(device));
-  return run_to_host(s, dc, wl, n, xyza_out, class_out, status_out, aux, stats);
+  return run_to_host(s, dc, wl, n, nullptr, xyza_out, class_out, status_out, aux, stats);
 }
 
 int grt_set_sub_chunk(uint64_t sub_rays) {

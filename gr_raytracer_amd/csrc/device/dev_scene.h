@@ -117,6 +117,13 @@ struct WorkList {
   // offsets mode, count decided on the device (the adaptive pass): the items actually
   // present are min(*n_live, n_items); n_items is the launch's capacity (NULL = n_items)
   const unsigned long long* n_live;
+  // Two-ended queue (probe-ordered traces, n_items < 2^31): the work counter packs the
+  // items claimed from the front (low 32 bits) and from the back (high 32 bits).  Of
+  // the waves sharing a SIMD, the one in an even hardware wave slot takes the longest
+  // predicted items from the front at raised issue priority; the others take the
+  // shortest from the back (integrate_kernel).
+  uint32_t two_ended;
+  uint32_t _pad;
 };
 
 // Window candidates of a ray beyond its GRT_WS_SLOTS workspace slots (the reference keeps

@@ -46,9 +46,6 @@ namespace grt {
 #ifndef GRT_KLDS_GEOMS
 #define GRT_KLDS_GEOMS (1 << GRT_GEOM_KERR)  // integrate kernels whose RKF stages k1..k4 live in LDS
 #endif
-#ifndef GRT_LONG_PRIO
-#define GRT_LONG_PRIO 0  // Kerr-Schild: issue priority for waves holding a ray past this many steps (0 = off)
-#endif
 #ifndef GRT_SINCOS_B
 #define GRT_SINCOS_B 1  // Schwarzschild / KerrBL RHS: wave-uniform straight-line sincos (region B)
 #endif
@@ -1515,6 +1512,12 @@ GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopSt
 GDEV unsigned long long load_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Items claimed so far from the work counter (both ends of a two-ended queue).
+GDEV uint64_t items_claimed(unsigned long long w, bool two_ended) {
+  return two_ended ? (w & 0xffffffffull) + (w >> 32) : w;
+}
+// This wave's hardware slot on its SIMD (HW_REG_HW_ID bits 3:0, gfx9).
+GDEV unsigned hw_wave_slot() { return __builtin_amdgcn_s_getreg(4 | (3 << 11)); }
 // One lane integrates one ray at a time: RKF45 attempts, and after every accepted
 // step the chord test of window (previous step, step) against every object in config
 // order (objects.rs:81) and the stop test (window_pass, should_stop).
@@ -1538,13 +1541,23 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   constexpr int NKL = (((GRT_KLDS_GEOMS) >> G) & 1) ? GRT_KL_STAGES : 0;
   if (tail_on && blockIdx.x == 0 && threadIdx.x == 0) tl.ctl[3] = __builtin_amdgcn_s_memrealtime();
 
+  // Two-ended queue (WorkList::two_ended).  The issue arbiter of a SIMD serves the oldest
+  // wave first: with two Kerr-Schild waves per SIMD the older one runs an attempt in
+  // ~31 us and the younger one in ~130 us while both are busy (per-ray record of a C4
+  // shard, profiles/r04a).  So one wave per SIMD (even hardware slot) takes the items
+  // with the longest predicted rays from the front and holds the issue priority
+  // explicitly (s_setprio), and the others take the shortest items from the back.  Both
+  // ends advance one packed counter, so a claim sees every earlier claim of either end:
+  // with (front, back) its snapshot, rank r is item front + r or n - 1 - (back + r), and
+  // exists while front + back + r < n.
+  const bool two_ended = wl.two_ended != 0;
+  const bool from_back = two_ended && (hw_wave_slot() & 1u);
+  if (two_ended && !from_back) __builtin_amdgcn_s_setprio(1);
   uint64_t chunk_next = 0, chunk_end = 0;  // wave-uniform work cursor
   bool active = false, done = false;
   bool started = false, ended = false;  // since the last live-count update (tail_on)
   uint32_t poll = 0;
   bool q_drained = false;  // this wave has seen the tile queue drained (it stays drained)
-  bool prio_high = false;  // GRT_LONG_PRIO: this wave's s_setprio level (wave-uniform)
-  (void)prio_high;
   uint64_t idx = 0;      // output slot of the current ray
   double y[8];           // state
   double c[3];           // Cartesian position of the last accepted step (when c_valid)
@@ -1575,15 +1588,20 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       // with 1e6-step rays must not sit on unstarted items of a 64-item chunk (they would
       // start only when one of its lanes frees up, possibly after the whole queue ran).
       // Its rays are long, so the extra atomics are rare.
-      const uint64_t take = TAIL ? cnt - remaining : CHUNK;
+      // A two-ended queue's claims are exact as well (remaining stays 0).
+      const uint64_t take = (TAIL || two_ended) ? cnt - remaining : CHUNK;
       if (cnt > remaining) {
         unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(counter, (unsigned long long)take);
+        if (lane == 0) b = atomicAdd(counter, from_back ? (unsigned long long)take << 32 : (unsigned long long)take);
         new_base = __shfl(b, 0);
       }
       if (need) {
         uint64_t rank = __popcll(need_mask & lanemask_lt);
         uint64_t item = rank < remaining ? chunk_next + rank : new_base + (rank - remaining);
+        if (two_ended) {  // new_base is the counter's snapshot (front | back << 32)
+          const uint64_t f = new_base & 0xffffffffull, bk = new_base >> 32;
+          item = (f + bk + rank >= n_items) ? n_items : (from_back ? n_items - 1 - (bk + rank) : f + rank);
+        }
         if (item >= n_items) {
           if (TAIL && tail_on && !done && tl.ctl[4] == 0ull)
             atomicCAS(&tl.ctl[4], 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1660,7 +1678,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         // drained test (an agent-scope load, served beyond this XCD's L2) runs every 256
         // attempts until the wave has seen the queue drained, then the live count every 16
         if ((chunk_next >= chunk_end || chunk_next >= n_items) && ((++poll & (q_drained ? 15u : 255u)) == 0u) &&
-            (q_drained || (q_drained = load_agent(counter) >= n_items)) &&
+            (q_drained || (q_drained = items_claimed(load_agent(counter), two_ended) >= n_items)) &&
             (long long)load_agent(&tl.ctl[0]) <= (long long)tl.threshold) {
           const uint64_t ev = __ballot(active);
           if (ev) {
@@ -1697,18 +1715,6 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       }
     }
     if (__ballot(!done) == 0) break;
-#if GRT_LONG_PRIO
-    if constexpr (TAIL) {
-      // waves that carry a long ray (past GRT_LONG_PRIO accepted steps) take VALU issue
-      // priority over their SIMD partner: the frame ends on those rays, not on the others
-      const bool long_wave = __ballot(active && i > (uint64_t)GRT_LONG_PRIO) != 0;
-      if (long_wave != prio_high) {
-        if (long_wave) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        prio_high = long_wave;
-      }
-    }
-#endif
     if (!active) continue;
 
     // ---------------- one RKF45 attempt (runge_kutta.rs:148-178) ----------------
@@ -2145,7 +2151,11 @@ hipError_t launch_health(int geometry, const DevScene* d_scene, const WorkList& 
 // heavy-tailed where rays spiral into the horizon or orbit near the photon sphere
 // (C4: 6% of the rays carry 60% of the steps, up to max_steps each); with the counts
 // the host queues the long tiles first, so the frame does not end on a lone ray that
-// started late.  Writes the steps taken (cap if the probe had not finished).
+// started late.  Writes the steps taken, or for a probe still going at the cap a key
+// above every finished count: cap + 1e8 / r, r its radial coordinate there.  Among the
+// capped probes of a C4 shard the radius at the cap predicts the ray's length (log-log
+// correlation -0.97, profiles/r04a: the long rays are the ones that climb out of the
+// hole's neighbourhood slowest), so the longest tiles are queued first.
 template <int G>
 __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ Sp, WorkList wl, uint32_t n_tiles,
                                                    uint32_t cap, uint32_t* __restrict__ steps_out) {
@@ -2177,7 +2187,16 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
     bool c_valid = false;
     if (should_stop<G>(S, y, cc, c_valid, i) != GRT_STOP_NONE) break;
   }
-  steps_out[t] = (uint32_t)(i < end ? i : cap);
+  uint32_t key = (uint32_t)i;
+  if (i >= end) {
+    double r;
+    if constexpr (G == GRT_GEOM_KERR) r = sqrt(ks_r_sqr(S.a, y[1], y[2], y[3]));
+    else if constexpr (G == GRT_GEOM_EUCLIDEAN) r = sqrt(y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+    else r = fabs(y[1]);
+    const double extra = 1e8 / fmax(r, 1e-3);
+    key = cap + (uint32_t)fmin(extra, (double)(0xffffffffu - cap));
+  }
+  steps_out[t] = key;
 }
 
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,

@@ -20,8 +20,10 @@ bool future_directed(int geometry, double radius, double a, const double positio
 double inner(int geometry, double radius, double a, const double position[4], const double v[4], const double w[4]);
 double signature0(int geometry);
 double r_isco(double r_s, double a);
+// log (nullable): the reference's info! lines of KerrTemperatureComputer::new
+// (temperature.rs:55-102), appended one per line
 int kerr_temperature_lut(double temperature, double outer_radius, double a, double radius, uint32_t n,
-                         double* lut_r, double* lut_t, double* r_isco_out);
+                         double* lut_r, double* lut_t, double* r_isco_out, std::string* log = nullptr);
 void blackbody_xyz(double temperature, double redshift, double out[3]);
 int blackbody_lut(uint32_t n, double* log_t, double* xyz);
 double inv_compand_srgb(double u);

@@ -31,6 +31,7 @@ struct grt_host_scene {
   std::vector<double> lut_r[GRT_MAX_OBJECTS], lut_t[GRT_MAX_OBJECTS];
   std::vector<double> bb_log_t, bb_xyz;
   std::string error;
+  std::string info_log;  // the reference's info! lines of the scene setup, one per line
 };
 
 namespace grt_host {
@@ -439,8 +440,8 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
         hs->lut_r[k].resize(1000);
         hs->lut_t[k].resize(1000);
         double spin = d.geometry == GRT_GEOM_SCHWARZSCHILD ? 0.0 : d.a;
-        if (grt_kerr_temperature_lut(temperature, o.outer_radius, spin, d.radius, 1000, hs->lut_r[k].data(),
-                                     hs->lut_t[k].data(), &o.r_isco))
+        if (grt_host::kerr_temperature_lut(temperature, o.outer_radius, spin, d.radius, 1000, hs->lut_r[k].data(),
+                                           hs->lut_t[k].data(), &o.r_isco, &hs->info_log))
           return fail(oname + " temperature LUT: DenominatorCloseToZero / NoCircularOrbitPossible");
         o.lut_r = hs->lut_r[k].data();
         o.lut_t = hs->lut_t[k].data();
@@ -466,6 +467,7 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
 }
 
 const grt_scene_desc* grt_host_scene_desc(const grt_host_scene* s) { return s ? &s->desc : nullptr; }
+const char* grt_host_scene_log(const grt_host_scene* s) { return s ? s->info_log.c_str() : ""; }
 void grt_host_scene_adaptive(const grt_host_scene* s, grt_adaptive_config* out) {
   if (s && out) *out = s->adaptive;
 }

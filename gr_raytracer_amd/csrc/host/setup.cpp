@@ -699,11 +699,19 @@ struct KerrTemp {  // temperature.rs:29-193
 }  // namespace
 
 int kerr_temperature_lut(double temperature, double outer_radius, double a, double radius, uint32_t n,
-                         double* lut_r, double* lut_t, double* r_isco_out) {
+                         double* lut_r, double* lut_t, double* r_isco_out, std::string* log) {
   double a_abs = std::fabs(a);
   double ri = r_isco(radius, a_abs);
   double eff_outer = outer_radius;
-  if (outer_radius <= ri) eff_outer = ri + std::fmax(1e-6, std::fabs(ri) * 1e-9);
+  if (outer_radius <= ri) {
+    eff_outer = ri + std::fmax(1e-6, std::fabs(ri) * 1e-9);
+    if (log)
+      *log += "outer_radius (" + rust_display_f64(outer_radius) + ") <= r_isco (" + rust_display_f64(ri) +
+              "); clamping to " + rust_display_f64(eff_outer) + " for stable LUT construction.\n";
+  }
+  if (log)
+    *log += "Computed r_isco: " + rust_display_f64(ri) + " from a: " + rust_display_f64(a_abs) +
+            " and radius: " + rust_display_f64(radius) + "\n";
   KerrTemp kt{a_abs, radius, ri, 1.0};
   double max_f = 0.0, max_r = 0.0;
   double dr = (eff_outer - ri) / (double)10;
@@ -717,6 +725,7 @@ int kerr_temperature_lut(double temperature, double outer_radius, double a, doub
       max_r = r;
     }
   }
+  if (log) *log += "Max f: " + rust_display_f64(max_f) + " at radius: " + rust_display_f64(max_r) + "\n";
   double integral, pre;
   int rc;
   if ((rc = kt.compute_integral(max_r, &integral))) return rc;
@@ -725,6 +734,9 @@ int kerr_temperature_lut(double temperature, double outer_radius, double a, doub
   double sigma_sb = 1.0;
   double f = sigma_sb * std::pow(temperature, 4.0);
   kt.m_dot = f / (coefficient * pre * integral);
+  if (log)
+    *log += "Computed m_dot: " + rust_display_f64(kt.m_dot) + " for target temperature: " +
+            rust_display_f64(temperature) + "\n";
   double step = (eff_outer - ri) / (double)(n - 1);
   for (uint32_t i = 0; i < n; ++i) {
     double r = ri + (double)i * step;

@@ -112,7 +112,7 @@ def main(argv=None) -> int:
 
     from . import _lib as L
     from .distributed import render_frame_adaptive
-    from .scene import GlobalOpts, load_scene
+    from .scene import GlobalOpts, coordinate_system_debug, duration_debug_2, load_scene
 
     if "WORLD_SIZE" not in os.environ:  # plain `python -m`: a world of one
         os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
@@ -135,6 +135,17 @@ def main(argv=None) -> int:
                           theta=a.theta, psi=a.psi, tone_mapping=a.tone_mapping,
                           show_sampling_mask=a.show_sampling_mask, sampling_mask_color=a.sampling_mask_color)
         scene = load_scene(a.config_file, opts, a.resource_root)
+        if rank == 0:
+            hs = scene._keep  # main.rs:100-103, then the scene setup's lines (temperature.rs:55-102)
+            _log(f"[render_dist] INFO Using coordinate system: {coordinate_system_debug(hs.desc.geometry, hs.desc.a)}")
+            for line in hs.info_log:
+                _log(f"[render_dist] INFO {line}")
+            if a.filename.endswith(".hdr"):  # raytracer.rs:468-469, :481-483
+                _log("[render_dist] INFO Creating HDR image")
+            else:
+                _log("[render_dist] INFO Creating non-HDR image")
+                _log(f"[render_dist] INFO Tone mapping method: "
+                     f"{ {'reinhard': 'Reinhard', 'global-linear': 'GlobalLinear'}[a.tone_mapping] }")
         mask = None
         if a.show_sampling_mask:
             mask = np.zeros(4)
@@ -152,7 +163,7 @@ def main(argv=None) -> int:
         supersampled = bool(cfg.enabled) or mask is not None
         if supersampled and rank == 0:  # raytracer.rs:264-267
             _log(f"[render_dist] INFO Rendering section from (0, 0) to ({scene.rows}, {scene.cols}) with supersampling")
-        for attempt in range(2):
+        for attempt in range(3):
             fails = L.SubsampleFailures(fail_cap, L.ptr(f_pix, C.c_uint32), L.ptr(f_smp, C.c_uint32),
                                         L.ptr(f_st, C.c_uint8), 0, L.ptr(f_stop, C.c_uint8), L.ptr(f_steps, C.c_uint32))
             report = {}
@@ -166,6 +177,12 @@ def main(argv=None) -> int:
             lost = stats[3:4].clone() if dist.get_backend() != "gloo" else stats[3:4].cpu()
             dist.all_reduce(lost)
             if int(lost[0]) == 0:
+                break
+            if attempt == 2:  # the pool cannot hold them (2^31 records): the frame is incomplete
+                if rank == 0:
+                    _log(f"[render_dist] ERROR {int(lost[0])} pixels lost hit candidates after growing the device "
+                          "hit pool twice; they are written without their candidates past the first "
+                          f"{L.GRT_MAX_HITS}")
                 break
             if rank == 0:
                 _log(f"[render_dist] WARN {int(lost[0])} pixels lost hit candidates (device hit pool full); "
@@ -227,7 +244,8 @@ def main(argv=None) -> int:
         steps = int(totals[0])
         _log(f"[render_dist] {world} GPU(s): {int(totals[2])} rays, {steps} accepted steps, {int(totals[1])} attempts, "
               f"{n_sel} supersampled pixels, frame {t_render:.3f} s ({steps / t_render:.3e} steps/s)")
-        _log(f"saved image to {a.filename}\nElapsed time: {time.perf_counter() - t_start:.3f} s")
+        _log(f"[render_dist] INFO saved image to {a.filename}")  # raytracer.rs:494, main.rs:175-176
+        _log(f"[render_dist] INFO Elapsed time: {duration_debug_2(time.perf_counter() - t_start)}")
         return 0
     finally:
         dist.destroy_process_group()

@@ -84,6 +84,12 @@ class HostScene:
         return L.lib().grt_host_scene_desc(self._h)
 
     @property
+    def info_log(self) -> list:
+        """The reference's info-level lines of the scene setup, in order (grt_host_scene_log:
+        the temperature LUT's, temperature.rs:55-102)."""
+        return [x for x in (L.lib().grt_host_scene_log(self._h) or b"").decode().split("\n") if x]
+
+    @property
     def adaptive(self) -> L.AdaptiveConfig:
         c = L.AdaptiveConfig()
         L.lib().grt_host_scene_adaptive(self._h, C.byref(c))
@@ -348,6 +354,13 @@ class Scene:
                 "slot": slot[:k], "step": step[:k]}
 
 
+def set_two_ended(on: bool = True) -> None:
+    """Probe-ordered traces take the tile queue from both ends (grt_set_two_ended): the
+    priority wave of each SIMD the longest tiles, the others the shortest.  Scheduling
+    only; results are identical in both modes."""
+    L.check(L.lib().grt_set_two_ended(1 if on else 0), "grt_set_two_ended")
+
+
 def set_tail(threshold: int = -1) -> None:
     """Long-ray hand-off of Kerr-Schild traces (grt_set_tail): -1 auto, 0 off, > 0 the
     live-ray threshold.  Scheduling only; results are identical in every mode."""
@@ -431,6 +444,39 @@ def format_f64(v: float) -> str:
     buf = C.create_string_buffer(1200)
     L.lib().grt_format_f64(float(v), buf, 1200)
     return buf.value.decode()
+
+
+def format_f64_debug(v: float) -> str:
+    """Rust's Debug of an f64 ({:?}): Display's digits with ".0" on integral values, and
+    exponential notation outside 1e-4 <= |v| < 1e16."""
+    import math
+    if math.isnan(v) or math.isinf(v):
+        return format_f64(v)
+    if v != 0.0 and (abs(v) < 1e-4 or abs(v) >= 1e16):
+        m, e = repr(float(v)).lower().split("e") if "e" in repr(float(v)).lower() else (repr(float(v)), "0")
+        return f"{m.rstrip('0').rstrip('.') if '.' in m else m}e{int(e)}"
+    d = format_f64(v)
+    return d if "." in d else d + ".0"
+
+
+def coordinate_system_debug(geometry: int, a: float) -> str:
+    """CoordinateSystem's Debug form for a geometry (geometry/*.rs coordinate_system, point.rs:11)."""
+    if geometry in (L.GEOM_SCHWARZSCHILD, L.GEOM_EUCLIDEAN_SPHERICAL):
+        return "Spherical"
+    if geometry == L.GEOM_KERR_BL:
+        return f"BoyerLindquist {{ a: {format_f64_debug(a)} }}"
+    return "Cartesian"
+
+
+def duration_debug_2(secs: float) -> str:
+    """A Duration's Debug form with two decimals ({:.2?}): the largest of s / ms / us / ns
+    with a non-zero integer part, the dropped digits rounded half up."""
+    ns = int(round(secs * 1e9))
+    for div, unit in ((10 ** 9, "s"), (10 ** 6, "ms"), (10 ** 3, "\u00b5s")):
+        if ns >= div:
+            h = (ns * 100 + div // 2) // div
+            return f"{h // 100}.{h % 100:02d}{unit}"
+    return f"{ns}.00ns"
 
 
 def r_isco(radius: float, a: float) -> float:

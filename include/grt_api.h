@@ -83,10 +83,11 @@ enum grt_status {
   GRT_ERR_BELOW_RISCO = 3,           /* temperature.rs:204-217                          */
   GRT_ERR_NON_FINITE_RADIUS = 4,     /* temperature.rs:199-202                          */
   GRT_FLAG_HIT_OVERFLOW = 0x80       /* the device hit pool was full: this ray's candidates
-                                        past GRT_MAX_HITS are missing.  Only the *_async
-                                        calls can return it (grt_hit_pool_reserve, then
-                                        trace again); the synchronous calls grow the pool
-                                        and trace again by themselves.                   */
+                                        past GRT_MAX_HITS are missing.  The *_async
+                                        calls return it (grt_hit_pool_reserve, then trace
+                                        again); the synchronous calls trace the flagged
+                                        pixels again, growing the pool to their need, and
+                                        return it only past 2^31 - 1 records.            */
 };
 
 /* Stop reason of the integration (integrator.rs:22-27), recorded per pixel. */
@@ -244,6 +245,11 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root,
 int grt_host_geometry_load(const char* toml_path, const grt_global_opts* opts,
                            grt_host_scene** out);
 const grt_scene_desc* grt_host_scene_desc(const grt_host_scene* s);
+/* The info-level lines the reference logs while it builds this scene, one per line, in
+ * order (today the temperature LUT's, KerrTemperatureComputer::new, temperature.rs:55-102:
+ * the r_isco clamp, "Computed r_isco: ...", "Max f: ...", "Computed m_dot: ..."; numbers
+ * in Rust's f64 Display form).  Owned by the scene; "" when there are none. */
+const char* grt_host_scene_log(const grt_host_scene* s);
 void grt_host_scene_adaptive(const grt_host_scene* s, grt_adaptive_config* out);
 int grt_host_scene_destroy(grt_host_scene* s);
 
@@ -311,7 +317,8 @@ typedef struct grt_stats {
   uint64_t accepted_steps; /* iterations of integrator.rs:100 that produced a step     */
   uint64_t attempts;       /* rkf45_step evaluations (6 RHS each)                      */
   uint64_t rays;
-  uint64_t hit_overflows;  /* pixels flagged GRT_FLAG_HIT_OVERFLOW (0 for the sync calls)     */
+  uint64_t hit_overflows;  /* pixels flagged GRT_FLAG_HIT_OVERFLOW: for the synchronous calls
+                              0 unless the pool would need more than 2^31 - 1 records     */
   double kernel_ms;        /* hipEvent time of the integration kernel(s)               */
   /* VolumetricDisc raymarches (volumetric_disc.rs:199-328): one per window-nearest
    * volumetric intersection whose colour reaches the composite, and their samples. */
@@ -433,9 +440,10 @@ int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt
 
 /* The device hit pool that keeps the window candidates past a ray's GRT_MAX_HITS slots
  * (no reference counterpart: the reference's per-ray Vec grows, scene.rs:139-152).
- * The pool grows on its own to half the rays of a trace; a trace that needs more flags
- * the pixels it could not keep (GRT_FLAG_HIT_OVERFLOW, grt_stats.hit_overflows).  The
- * synchronous calls then grow it and trace again.  After an *_async call whose
+ * A trace starts with the pool at its minimum (grt_set_hit_pool_min, 2^20 records) or
+ * the size a measured need grew it to; a trace that needs more flags the pixels it could
+ * not keep (GRT_FLAG_HIT_OVERFLOW, grt_stats.hit_overflows).  The synchronous calls then
+ * trace those pixels again (growing the pool to their need).  After an *_async call whose
  * d_stats[3] is non-zero, call this with records = 0 (waits for the device, then sizes
  * the pool for the largest trace since the last call) or with an explicit record count,
  * and trace again.  *capacity (nullable) returns the pool size in records. */
@@ -589,6 +597,11 @@ int grt_set_launch_config(int blocks_per_cu, int threads_per_block);
  * max_steps >= 262144 over >= 1024 tiles; KerrBL's Mino-time rays are all short).
  * Scheduling only: every pixel's result is identical in all modes. */
 int grt_set_schedule(int mode);
+/* Probe-ordered traces (above) hand the queue out from both ends: on every SIMD the wave
+ * in an even hardware slot takes the tiles with the longest predicted rays, at raised
+ * issue priority, the others take the shortest (1 = default); 0 = one end, longest
+ * first, for every wave.  Scheduling only: results are identical in both modes. */
+int grt_set_two_ended(int on);
 /* Long-ray hand-off of Kerr-Schild traces: once the tile queue is drained and at most
  * `threshold` rays are still integrating, they continue in a tail kernel that splits each
  * RHS evaluation over 4 lanes (one wave per SIMD).  -1 = automatic (default: on, threshold

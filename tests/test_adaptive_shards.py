@@ -361,3 +361,38 @@ def test_cli_logs_unterminated_rays_like_the_reference(grt, oracle, gpu, tmp_pat
     assert d.returncode == 0, d.stderr[-3000:]
     assert events(d.stderr) == sorted(want)
     assert re.findall(r"INFO Supersampling (\d+) pixels", d.stderr) == [str(int(sel.sum()))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fname,geom", [("o.png", "kerr.toml"), ("o.hdr", "kerr-bl.toml")])
+def test_cli_info_lines_follow_the_reference(grt, oracle, gpu, tmp_path, fname, geom):
+    """`grt render` with a stock TOML logs the reference's info! lines in its order:
+    main.rs:100-103 (coordinate system), the temperature LUT's (temperature.rs:63-102:
+    r_isco from the oracle's own restatement, in Rust's Display form), raytracer.rs:468-483
+    (HDR or non-HDR, tone mapping), :264-267 / :325 / :313-316 (the supersampled section),
+    :494 (saved image) and main.rs:176 (elapsed time, Duration's {:.2?})."""
+    import re
+
+    from gr_raytracer_amd.scene import format_f64
+
+    out = tmp_path / fname
+    flags = ["--width=24", "--height=16", "--max-steps=500", "--camera-position=-10,0,-0.5", "--config-file",
+             str(SCENES / geom), "--resource-root", str(RESOURCES)]
+    r = subprocess.run([str(ROOT / "gr_raytracer_amd" / "lib" / "grt"), *flags, "render", "--filename", str(out)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    info = [ln.split(" INFO ", 1)[1] for ln in r.stderr.splitlines() if " INFO " in ln]
+    a, radius = 0.499, 1.0
+    coord = "Cartesian" if geom == "kerr.toml" else "BoyerLindquist { a: 0.499 }"
+    want = [f"Using coordinate system: {coord}",
+            f"Computed r_isco: {format_f64(oracle.r_isco(radius, a))} from a: 0.499 and radius: 1",
+            r"Max f: [0-9.]+ at radius: [0-9.]+",
+            r"Computed m_dot: [0-9.]+ for target temperature: 2000"]
+    want += ["Creating HDR image"] if fname.endswith(".hdr") else ["Creating non-HDR image",
+                                                                     "Tone mapping method: Reinhard"]
+    want += [r"Rendering section from \(0, 0\) to \(16, 24\) with supersampling", r"Supersampling \d+ pixels",
+             r"Finished rendering section from \(0, 0\) to \(16, 24\)", f"saved image to {re.escape(str(out))}",
+             r"Elapsed time: \d+\.\d\d(s|ms)"]
+    assert len(info) == len(want), info
+    for got, pat in zip(info, want):
+        assert re.fullmatch(pat if "\\" in pat or "[" in pat else re.escape(pat), got), (got, pat)

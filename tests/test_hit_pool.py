@@ -84,9 +84,11 @@ def test_late_window_errors(grt, oracle, gpu):
 
 @pytest.mark.gpu
 def test_full_pool(grt, gpu):
-    """A pool too small for the trace: the synchronous call grows it and traces again
-    (bit-identical to a roomy pool); an async call flags exactly the pixels whose
-    candidates it lost, and after grt_hit_pool_reserve the same call is complete."""
+    """A pool too small for the trace: the synchronous call traces again only the pixels
+    that lost candidates, growing the pool to their need (bit-identical to a roomy pool,
+    and the extra rays are a subset of the heavy pixels); an async call flags exactly the
+    pixels whose candidates it lost, and after grt_hit_pool_reserve the same call is
+    complete."""
     import torch
 
     from test_gpu_parity import _desc_ptr
@@ -100,10 +102,36 @@ def test_full_pool(grt, gpu):
     want_xyza, want_status = roomy.xyza[sel], roomy.status[sel]
     L.check(L.lib().grt_set_hit_pool_min(64))
     try:
-        sc = grt.Scene(_desc_ptr(d), keepalive=d)  # a fresh device copy: a 288-record pool
-        sync = sc.render_pixels(*rect)
+        sc = grt.Scene(_desc_ptr(d), keepalive=d)  # a fresh device copy: a 64-record pool
+        sync = sc.render_pixels(*rect, aux=True)
         assert np.array_equal(sync.xyza, want_xyza) and np.array_equal(sync.status, want_status)
+        assert np.array_equal(sync.xyza64, roomy.xyza64[sel]) and np.array_equal(sync.hits, roomy.hits[sel])
+        assert np.array_equal(sync.steps, roomy.steps[sel]) and np.array_equal(sync.stop_reason, roomy.stop_reason[sel])
         assert sync.stats["hit_overflows"] == 0
+        n_rect = rect[2] * rect[3]
+        heavy = roomy.hits[sel] > L.GRT_MAX_HITS
+        # the first trace plus re-traces of flagged (hence heavy) pixels only, each at most
+        # three times (fits / grows the pool to the subset's need / fits)
+        assert n_rect < sync.stats["rays"] <= n_rect + 3 * heavy.sum(), (sync.stats["rays"], heavy.sum())
+
+        # a row-band shard (band 8, shard 1 of 3) and an offsets list re-trace their flagged
+        # pixels too: frame rows of the shard's local rows, the same (pixel, dx, dy) items
+        shard = grt.Scene(_desc_ptr(d), keepalive=d).render_shard(8, 1, 3, aux=True)
+        lr = np.arange(shard.steps.size // N)
+        fr = ((lr // 8) * 3 + 1) * 8 + lr % 8
+        rows_sel = (np.arange(N * N) // N)
+        pick = np.concatenate([np.flatnonzero(rows_sel == r) for r in fr])
+        assert np.array_equal(shard.xyza64, roomy.xyza64[pick]) and np.array_equal(shard.status, roomy.status[pick])
+        assert shard.stats["hit_overflows"] == 0 and shard.stats["rays"] > shard.steps.size
+        rng = np.random.default_rng(7)
+        pix = np.flatnonzero(sel).astype(np.uint32)
+        offs = (pix, rng.random(pix.size), rng.random(pix.size))
+        L.check(L.lib().grt_set_hit_pool_min(1 << 20))
+        want_off = grt.Scene(_desc_ptr(d), keepalive=d).render_pixels(0, 0, N, N, offsets=offs)
+        L.check(L.lib().grt_set_hit_pool_min(64))
+        got_off = grt.Scene(_desc_ptr(d), keepalive=d).render_pixels(0, 0, N, N, offsets=offs)
+        assert np.array_equal(got_off.xyza64, want_off.xyza64) and np.array_equal(got_off.status, want_off.status)
+        assert got_off.stats["rays"] > pix.size and want_off.stats["rays"] == pix.size
 
         sc2 = grt.Scene(_desc_ptr(d), keepalive=d)
         n = rect[2] * rect[3]
@@ -123,12 +151,11 @@ def test_full_pool(grt, gpu):
         x1, s1, lost = run()
         flagged = (s1 & L.FLAG_HIT_OVERFLOW) != 0
         assert lost == flagged.sum() > 0
-        heavy = roomy.hits[sel] > L.GRT_MAX_HITS
         assert not np.any(flagged & ~heavy)
         assert np.array_equal(x1[~flagged], want_xyza[~flagged])
         cap = C.c_uint64()
         L.check(L.lib().grt_hit_pool_reserve(sc2._s, 0, 0, C.byref(cap)), "grt_hit_pool_reserve")
-        assert cap.value > 288
+        assert cap.value > 64
         x2, s2, lost2 = run()
         assert lost2 == 0 and np.array_equal(x2, want_xyza) and np.array_equal(s2, want_status)
     finally:

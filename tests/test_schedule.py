@@ -18,17 +18,21 @@ def test_probe_order_is_result_neutral(grt, gpu, toml, mk, rect, max_steps):
     hs = host_scene(grt, toml, mk(grt, max_steps=max_steps))
     sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
     out = {}
-    try:
-        for mode in (0, 1):
+    try:  # row-major tiles; probe order from one end; probe order from both ends (default)
+        for mode, two in ((0, 1), (1, 0), (1, 1)):
             L.check(L.lib().grt_set_schedule(mode))
-            out[mode] = sc.render_pixels(*rect, device=gpu)
+            L.check(L.lib().grt_set_two_ended(two))
+            out[mode, two] = sc.render_pixels(*rect, device=gpu)
     finally:
         L.lib().grt_set_schedule(-1)
-    a, b = out[0], out[1]
-    assert np.array_equal(a.xyza64, b.xyza64) and np.array_equal(a.xyza, b.xyza)
-    assert np.array_equal(a.ray_class, b.ray_class) and np.array_equal(a.status, b.status)
-    assert np.array_equal(a.steps, b.steps) and np.array_equal(a.stop_reason, b.stop_reason)
-    assert a.stats["accepted_steps"] == b.stats["accepted_steps"] and a.stats["rays"] == b.stats["rays"]
+        L.lib().grt_set_two_ended(1)
+    a = out[0, 1]
+    for b in (out[1, 0], out[1, 1]):
+        assert np.array_equal(a.xyza64, b.xyza64) and np.array_equal(a.xyza, b.xyza)
+        assert np.array_equal(a.ray_class, b.ray_class) and np.array_equal(a.status, b.status)
+        assert np.array_equal(a.steps, b.steps) and np.array_equal(a.stop_reason, b.stop_reason)
+        assert np.array_equal(a.hits, b.hits)
+        assert a.stats["accepted_steps"] == b.stats["accepted_steps"] and a.stats["rays"] == b.stats["rays"]
 
 
 def test_schedule_mode_is_validated(grt):
@@ -36,3 +40,5 @@ def test_schedule_mode_is_validated(grt):
 
     with pytest.raises(L.GrtError):
         L.check(L.lib().grt_set_schedule(7))
+    with pytest.raises(L.GrtError):
+        L.check(L.lib().grt_set_two_ended(2))

@@ -17,6 +17,8 @@ import os  # noqa: E402
 from gr_raytracer_amd import _lib as L  # noqa: E402
 if "GRT_SCHEDULE" in os.environ:  # -1 auto, 0 row-major tiles, 1 probe-ordered
     L.check(L.lib().grt_set_schedule(int(os.environ["GRT_SCHEDULE"])))
+if "GRT_TWO_ENDED" in os.environ:  # 1 (default) both ends of the tile queue, 0 one end
+    L.check(L.lib().grt_set_two_ended(int(os.environ["GRT_TWO_ENDED"])))
 if "GRT_TAIL" in os.environ:  # -1 auto, 0 off, > 0 hand-off threshold
     L.check(L.lib().grt_set_tail(int(os.environ["GRT_TAIL"])))
 import hashlib  # noqa: E402
@@ -37,5 +39,6 @@ for s in shards:
                       "kernel_ms": st["kernel_ms"], "accepted": st["accepted_steps"], "attempts": st["attempts"],
                       "steps_per_s": st["accepted_steps"] / (st["kernel_ms"] * 1e-3),
                       "overflows": st["hit_overflows"], "schedule": os.environ.get("GRT_SCHEDULE", "auto"),
-                      "tail": os.environ.get("GRT_TAIL", "auto"), "handoffs": sc.tail_handoffs(), "tail_timeline": tail,
+                      "tail": os.environ.get("GRT_TAIL", "auto"),
+                      "two_ended": os.environ.get("GRT_TWO_ENDED", "1"), "handoffs": sc.tail_handoffs(), "tail_timeline": tail,
                       "md5": hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12]}), flush=True)
