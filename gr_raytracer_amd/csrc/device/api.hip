@@ -164,8 +164,9 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   const uint64_t M = GRT_WS_SLOTS;
   const bool vol = dc.vol;
   // volumetric scenes: rc grows to 6 doubles; chord directions, raymarched colours, jobs
-  const uint64_t per_ray = 8 * 8 + (vol ? 6 : 4) * 8 + 1 + 1 + 3 * 4 + 4 + M * (4 + 1 + 4 * 8 + 3 * 8) +
-                           (vol ? M * (3 * 8 + 4 * 8 + 8) : 0);
+  // final-state record (64 B), meta record (16 B), pool list ends (8 B), candidate slots;
+  // volumetric scenes: the ray constants (48 B), chord directions, raymarched colours, jobs
+  const uint64_t per_ray = 64 + 16 + 8 + M * (4 + 1 + 4 * 8 + 3 * 8) + (vol ? 6 * 8 + M * (3 * 8 + 4 * 8 + 8) : 0);
   // volumetric scenes: the raymarch job list also holds one job per pool record
   const uint64_t jobs_extra = vol ? dc.pool_cap : 0;
   if (n > dc.ws_cap || (vol && !dc.ws_vol) || jobs_extra > dc.ws_jobs_pool) {
@@ -193,15 +194,12 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
     return (void*)r;
   };
   ws->n = n;
-  ws->y = (double*)take(8 * 8 * cap);
-  ws->rc = (double*)take((vol ? 6 : 4) * 8 * cap);
+  ws->fin = (double*)take(64 * cap);
+  ws->meta = (uint32_t*)take(16 * cap);
+  ws->rc = vol ? (double*)take(6 * 8 * cap) : nullptr;
   ws->rec_p = (double*)take(4 * M * 8 * cap);
   ws->rec_pt = (double*)take(3 * M * 8 * cap);
-  ws->steps = (uint32_t*)take(4 * cap);
   ws->rec_win = (uint32_t*)take(M * 4 * cap);
-  ws->stop = (uint8_t*)take(cap);
-  ws->status = (uint8_t*)take(cap);
-  ws->nrec = (uint32_t*)take(4 * cap);
   dc.ws_head = (uint32_t*)take(4 * cap);
   dc.ws_last = (uint32_t*)take(4 * cap);
   ws->rec_obj = (uint8_t*)take(M * cap);
@@ -547,7 +545,7 @@ int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList*
       dc.tail_mem = nullptr;
     }
     dc.tail_cap = 0;
-    HIP_TRY(hipMalloc(&dc.tail_mem, cap * 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dc.tail_mem, cap * 17 * sizeof(unsigned long long)));
     dc.tail_cap = cap;
   }
   tl->ctl = dc.d_tail_ctl;
@@ -733,6 +731,29 @@ int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double t
 }
 
 #if GRT_RAY_TIMES
+// Diagnostic builds only (not in grt_api.h): the probe pass and tile order of a row-band
+// shard, without the trace: probe keys (n_tiles) and the queue order (n_tiles).
+int grt_debug_probe_order(grt_scene* s, int device, const grt_row_shard* sh, uint32_t* probe_out,
+                          uint32_t* order_out, uint64_t n_tiles) {
+  if (!s || !sh || !probe_out || !order_out) return fail(-EINVAL, "null argument");
+  DeviceCopy* dc;
+  int rc;
+  if ((rc = ensure_device(s, device, &dc))) return rc;
+  HIP_TRY(hipSetDevice(device));
+  grt::WorkList wl = rect_worklist(0, 0, grt_shard_row_count((uint32_t)s->desc.camera.rows, sh),
+                                   (uint32_t)s->desc.camera.cols);
+  wl.band_rows = sh->band_rows;
+  wl.shard = sh->shard;
+  wl.n_shards = sh->n_shards;
+  if (wl.n_items / 64 != n_tiles) return fail(-EINVAL, "tile count differs");
+  const uint32_t* order = nullptr;
+  if ((rc = enqueue_tile_order(s, *dc, wl, nullptr, &order))) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(probe_out, dc->sched_mem, n_tiles * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(order_out, order, n_tiles * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 // Diagnostic builds only (not in grt_api.h): the last trace's per-ray schedule record,
 // [6][n] words (start, hand-off, end, hardware place, integrate / tail attempts), and
 // the integrate kernel's start (s_memrealtime) in *t0.

@@ -155,19 +155,20 @@ struct HitPool {
                              //     HIT_NIL once one was lost
 };
 
-// Hand-off from the integrate kernel to the shade kernel, structure-of-arrays with
-// n = number of output slots of the launch.  Per ray: final state y[8], the per-ray
-// constants (observer energy, KerrBL E / L_z / Q), stop reason, status, step count
-// and its window candidates: the first GRT_WS_SLOTS in slots (slot-major: slot k of ray
-// i at k*n + i), the rest in the hit pool.
+// Hand-off from the integrate kernel to the shade kernel, n = number of output slots of
+// the launch.  Per ray, written once by the lane that ends it, as two records of whole
+// 16-B stores (a 64-B line and a quarter of one, instead of one 8-B store per field into
+// a structure-of-arrays slot: rays end one by one in probe order, so those lines were
+// written back part-filled): the final state and the constants the shade needs (fin,
+// layout in geodesic.hip fin_put), and the step count, candidate count, stop reason and
+// status (meta).  The window candidates: the first GRT_WS_SLOTS in slots (slot-major:
+// slot k of ray i at k*n + i), the rest in the hit pool.
 struct Workspace {
   uint64_t n;
-  double* y;          // [8][n]
-  double* rc;         // [4][n], [6][n] with volumetric objects (+ p_t, p_phi)
-  uint8_t* stop;      // [n]
-  uint8_t* status;    // [n]
-  uint32_t* nrec;     // [n] candidates recorded
-  uint32_t* steps;    // [n]
+  double* fin;        // [n][8] final-state record (64 B, 64-B aligned)
+  uint32_t* meta;     // [n][4] steps, candidates, stop | status << 8, 0
+  double* rc;         // volumetric scenes only: [6][n] ray constants (observer energy, E, L_z,
+                      // Q, p_t, p_phi) written at the ray's start, for the raymarch
   uint32_t* rec_win;  // [MAX][n] window (accepted-step) index
   uint8_t* rec_obj;   // [MAX][n] object index
   double* rec_p;      // [4][MAX][n] momentum lerped to the hit (objects.rs:27-44)
@@ -230,8 +231,8 @@ struct TailList {
   unsigned long long* ctl;  // 16 words
   uint64_t cap;             // entries of st (0: hand-off disabled)
   uint64_t threshold;       // hand off once the queue is drained and live <= threshold
-  // [16][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,
-  // nrec | retries << 32 | c_valid << 48
+  // [17][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,
+  // nrec | retries << 32 | c_valid << 48, observer energy
   unsigned long long* st;
 };
 

@@ -55,6 +55,9 @@ namespace grt {
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
+#ifndef GRT_FIN_CONST_AT_START
+#define GRT_FIN_CONST_AT_START 0  // write the ray constants into the final-state record at the ray's start
+#endif
 #ifndef GRT_RAY_TIMES
 #define GRT_RAY_TIMES 0  // diagnostic builds only: per-ray schedule record (tools/c4_ray_times.py)
 #endif
@@ -1340,7 +1343,6 @@ GDEV int step_control(const DevScene& S, double err_sq, double& h_cur, int& retr
   return STEP_ACCEPTED;
 }
 
-// End of a ray: its final state goes to the workspace for the shade kernel.
 #if GRT_RAY_TIMES
 // Per-ray schedule record of a diagnostic build, [6][n] words at output slot idx: start,
 // hand-off and end (s_memrealtime, 100 MHz), the starting lane's hardware place
@@ -1360,16 +1362,98 @@ hipError_t set_ray_times(unsigned long long* p) { return hipMemcpyToSymbol(HIP_S
 #define RAY_TIME(n, idx, k, v) ((void)0)
 #endif
 
-GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, int stop, int status, uint32_t nrec,
-                    uint32_t steps) {
-  const uint64_t n = ws.n;
-  RAY_TIME(n, idx, 2, __builtin_amdgcn_s_memrealtime());
+// The final-state record of a ray (Workspace::fin, 8 doubles): what the shade kernel reads
+// of the state and the ray constants.  KerrBL: r, theta, phi, v_r, v_theta, observer
+// energy, E, L_z (y[6], y[7] are identically 0, Q only drives the RHS); the other charts:
+// y[1..7] and the observer energy (y[0] is not read; Kerr-Schild's momentum needs none
+// of E, L_z, Q).
+template <int G>
+GDEV void fin_put(const Workspace& ws, uint64_t idx, const double* y, const RayConst& rc) {
+  double v[8];
+  if constexpr (G == GRT_GEOM_KERR_BL) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) ws.y[k * n + idx] = y[k];
-  ws.stop[idx] = (uint8_t)stop;
-  ws.status[idx] = (uint8_t)status;
-  ws.nrec[idx] = nrec;
-  ws.steps[idx] = steps;
+    for (int k = 0; k < 5; ++k) v[k] = y[1 + k];
+    v[5] = rc.obs;
+    v[6] = rc.e;
+    v[7] = rc.lz;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) v[k] = y[1 + k];
+    v[7] = rc.obs;
+  }
+  double2* d = reinterpret_cast<double2*>(ws.fin + idx * 8);
+#if GRT_FIN_CONST_AT_START
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    d[0] = make_double2(v[0], v[1]);
+    d[1] = make_double2(v[2], v[3]);
+    ws.fin[idx * 8 + 4] = v[4];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d[k] = make_double2(v[2 * k], v[2 * k + 1]);
+    ws.fin[idx * 8 + 6] = v[6];
+  }
+#else
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = make_double2(v[2 * k], v[2 * k + 1]);
+#endif
+}
+// The ray constants' part of the record, at the ray's start (GRT_FIN_CONST_AT_START)
+template <int G>
+GDEV void fin_put_const(const Workspace& ws, uint64_t idx, const RayConst& rc) {
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    ws.fin[idx * 8 + 5] = rc.obs;
+    reinterpret_cast<double2*>(ws.fin + idx * 8)[3] = make_double2(rc.e, rc.lz);
+  } else {
+    ws.fin[idx * 8 + 7] = rc.obs;
+  }
+}
+template <int G>
+GDEV void fin_get(const Workspace& ws, uint64_t idx, double* y, RayConst& rc) {
+  const double2* d = reinterpret_cast<const double2*>(ws.fin + idx * 8);
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double2 w = d[k];
+    v[2 * k] = w.x;
+    v[2 * k + 1] = w.y;
+  }
+  y[0] = 0.0;
+  rc.q = 0.0;
+  rc.pt = 0.0;
+  rc.pphi = 0.0;
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) y[1 + k] = v[k];
+    y[6] = 0.0;
+    y[7] = 0.0;
+    rc.obs = v[5];
+    rc.e = v[6];
+    rc.lz = v[7];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) y[1 + k] = v[k];
+    rc.obs = v[7];
+    rc.e = 0.0;
+    rc.lz = 0.0;
+  }
+}
+struct RayMeta {
+  uint32_t steps, nrec;
+  int stop, status;
+};
+GDEV RayMeta meta_get(const Workspace& ws, uint64_t idx) {
+  const uint4 m = reinterpret_cast<const uint4*>(ws.meta)[idx];
+  return RayMeta{m.x, m.y, (int)(m.z & 0xffu), (int)((m.z >> 8) & 0xffu)};
+}
+
+// End of a ray: its final state and counts go to the workspace for the shade kernel.
+template <int G>
+GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, const RayConst& rc, int stop, int status,
+                    uint32_t nrec, uint32_t steps) {
+  RAY_TIME(ws.n, idx, 2, __builtin_amdgcn_s_memrealtime());
+  fin_put<G>(ws, idx, y, rc);
+  reinterpret_cast<uint4*>(ws.meta)[idx] =
+      make_uint4(steps, nrec, (uint32_t)(stop & 0xff) | ((uint32_t)(status & 0xff) << 8), 0u);
 }
 
 // Candidate nrec >= GRT_WS_SLOTS of ray idx: one record appended to the hit pool and
@@ -1479,8 +1563,9 @@ struct LoopState {
   uint32_t nrec;
   int retries;
   bool c_valid;
+  double obs;  // observer energy (redshift.rs:40-43), for the final-state record
 };
-// Entry e of an entry arena `st` of m entries ([16][m] words: TailList::st / est).
+// Entry e of an entry arena `st` of m entries ([17][m] words: TailList::st).
 GDEV void tail_save(unsigned long long* st, uint64_t m, uint64_t e, const LoopState& s) {
   unsigned long long* w = st + e;
 #pragma unroll
@@ -1493,6 +1578,7 @@ GDEV void tail_save(unsigned long long* st, uint64_t m, uint64_t e, const LoopSt
   w[14 * m] = s.idx;
   w[15 * m] = (unsigned long long)s.nrec | ((unsigned long long)(uint32_t)s.retries << 32) |
               ((unsigned long long)(s.c_valid ? 1 : 0) << 48);
+  w[16 * m] = (unsigned long long)__double_as_longlong(s.obs);
 }
 GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopState& s) {
   const unsigned long long* w = st + e;
@@ -1508,6 +1594,7 @@ GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopSt
   s.nrec = (uint32_t)f;
   s.retries = (int)((f >> 32) & 0xffffu);
   s.c_valid = ((f >> 48) & 1u) != 0;
+  s.obs = __longlong_as_double((long long)w[16 * m]);
 }
 GDEV unsigned long long load_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1628,11 +1715,14 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
           }
           if (valid) {
             init_ray<G, VOL>(S, row, col, y, rc);
-            ws.rc[0 * n + idx] = rc.obs;
-            ws.rc[1 * n + idx] = rc.e;
-            ws.rc[2 * n + idx] = rc.lz;
-            ws.rc[3 * n + idx] = rc.q;
-            if constexpr (VOL) {
+#if GRT_FIN_CONST_AT_START
+            fin_put_const<G>(ws, idx, rc);
+#endif
+            if constexpr (VOL) {  // the raymarch's frequency data (march_kernel)
+              ws.rc[0 * n + idx] = rc.obs;
+              ws.rc[1 * n + idx] = rc.e;
+              ws.rc[2 * n + idx] = rc.lz;
+              ws.rc[3 * n + idx] = rc.q;
               ws.rc[4 * n + idx] = rc.pt;
               ws.rc[5 * n + idx] = rc.pphi;
             }
@@ -1651,7 +1741,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
             RAY_TIME(n, idx, 3, hw_place());
 #endif
             if (S.max_steps <= 1) {  // `for i in 1..max_steps` never runs
-              store_ray(ws, idx, y, GRT_STOP_NONE, GRT_OK, 0, 0);
+              store_ray<G>(ws, idx, y, rc, GRT_STOP_NONE, GRT_OK, 0, 0);
               active = false;
               ended = true;
             }
@@ -1703,6 +1793,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
                 s.nrec = nrec;
                 s.retries = retries;
                 s.c_valid = c_valid;
+                s.obs = rc.obs;
                 tail_save(tl.st, tl.cap, e, s);
                 RAY_TIME(n, idx, 1, __builtin_amdgcn_s_memrealtime());
                 RAY_TIME(n, idx, 4, ray_att);
@@ -1754,7 +1845,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     const int ctl = step_control(S, err_sq, h_cur, retries, h_next);
     if (ctl != STEP_ACCEPTED) {
       if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
-        store_ray(ws, idx, y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
+        store_ray<G>(ws, idx, y, rc, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)i);
         RAY_TIME(n, idx, 4, ray_att);
         active = false;
         ended = true;
@@ -1772,7 +1863,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
 
     int stop = should_stop<G>(S, y, c, c_valid, i);
     if (stop != GRT_STOP_NONE || i == S.max_steps - 1) {
-      store_ray(ws, idx, y, stop, GRT_OK, nrec, (uint32_t)i);
+      store_ray<G>(ws, idx, y, rc, stop, GRT_OK, nrec, (uint32_t)i);
       RAY_TIME(n, idx, 4, ray_att);
       active = false;
       ended = true;
@@ -1810,7 +1901,7 @@ GDEV bool quad_attempt(const DevScene& S, const Workspace& ws, const RayConst& r
   const int ctl = step_control(S, err_sq, s.h_cur, s.retries, h_next);
   if (ctl != STEP_ACCEPTED) {
     if (ctl == STEP_FAILED) {  // Err(MaxStepsReached)
-      if (writer) store_ray(ws, s.idx, s.y, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)s.i);
+      if (writer) store_ray<G>(ws, s.idx, s.y, rc, GRT_STOP_NONE, GRT_ERR_MAX_STEPS_REACHED, 0, (uint32_t)s.i);
       return true;
     }
     return false;
@@ -1823,7 +1914,7 @@ GDEV bool quad_attempt(const DevScene& S, const Workspace& ws, const RayConst& r
   for (int k = 0; k < 8; ++k) s.y[k] = yn[k];
   const int stop = should_stop<G>(S, s.y, s.c, s.c_valid, s.i);
   if (stop != GRT_STOP_NONE || s.i == S.max_steps - 1) {
-    if (writer) store_ray(ws, s.idx, s.y, stop, GRT_OK, s.nrec, (uint32_t)s.i);
+    if (writer) store_ray<G>(ws, s.idx, s.y, rc, stop, GRT_OK, s.nrec, (uint32_t)s.i);
     return true;
   }
   s.retries = 0;
@@ -1871,10 +1962,10 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
           done = true;
         } else {
           tail_load(tl.st, tl.cap, e, s);
-          rc.obs = ws.rc[0 * n + s.idx];
-          rc.e = ws.rc[1 * n + s.idx];
-          rc.lz = ws.rc[2 * n + s.idx];
-          rc.q = ws.rc[3 * n + s.idx];
+          rc.obs = s.obs;  // Kerr-Schild: the RHS and the momentum read no ray constant
+          rc.e = 0.0;
+          rc.lz = 0.0;
+          rc.q = 0.0;
           rc.pt = VOL ? ws.rc[4 * n + s.idx] : 0.0;
           rc.pphi = VOL ? ws.rc[5 * n + s.idx] : 0.0;
           active = true;
@@ -2152,10 +2243,12 @@ hipError_t launch_health(int geometry, const DevScene* d_scene, const WorkList& 
 // (C4: 6% of the rays carry 60% of the steps, up to max_steps each); with the counts
 // the host queues the long tiles first, so the frame does not end on a lone ray that
 // started late.  Writes the steps taken, or for a probe still going at the cap a key
-// above every finished count: cap + 1e8 / r, r its radial coordinate there.  Among the
-// capped probes of a C4 shard the radius at the cap predicts the ray's length (log-log
-// correlation -0.97, profiles/r04a: the long rays are the ones that climb out of the
-// hole's neighbourhood slowest), so the longest tiles are queued first.
+// above every finished count: cap + 2^30 (r - r_stop) / r_stop, r its radial coordinate
+// there and r_stop the horizon test's radius (cap alone without a horizon).  The capped
+// probes of a C4 shard all creep towards the horizon with steps of ~1e-8, and the
+// distance they have left predicts the ray's length (log-log correlation 0.98 with the
+// probe pixel's own count; the 300 tiles with a ray past 8e5 steps are among the 311
+// largest keys but 11; tools/c4_probe_features.py), so the longest tiles are queued first.
 template <int G>
 __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ Sp, WorkList wl, uint32_t n_tiles,
                                                    uint32_t cap, uint32_t* __restrict__ steps_out) {
@@ -2189,12 +2282,13 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
   }
   uint32_t key = (uint32_t)i;
   if (i >= end) {
-    double r;
-    if constexpr (G == GRT_GEOM_KERR) r = sqrt(ks_r_sqr(S.a, y[1], y[2], y[3]));
-    else if constexpr (G == GRT_GEOM_EUCLIDEAN) r = sqrt(y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
-    else r = fabs(y[1]);
-    const double extra = 1e8 / fmax(r, 1e-3);
-    key = cap + (uint32_t)fmin(extra, (double)(0xffffffffu - cap));
+    key = cap;
+    const bool horizon = G == GRT_GEOM_SCHWARZSCHILD || ((G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) && S.has_horizon);
+    if (horizon && S.horizon_r > 0.0) {
+      const double rad = (G == GRT_GEOM_KERR) ? sqrt(ks_r_sqr(S.a, y[1], y[2], y[3])) : y[1];
+      const double d = (rad - S.horizon_r) / S.horizon_r * 1073741824.0;
+      if (d > 0.0) key = cap + (uint32_t)fmin(d, (double)(0xffffffffu - cap));  // NaN: stays cap
+    }
   }
   steps_out[t] = key;
 }
@@ -2346,8 +2440,7 @@ struct RecRef {
 };
 // Candidates a ray can replay in order: all of them, unless its pool list was lost
 // (the pool was full), in which case only the workspace slots (*lost = true).
-GDEV uint32_t rec_count(const Workspace& ws, uint64_t idx, bool* lost) {
-  const uint32_t nrec = ws.nrec[idx];
+GDEV uint32_t rec_count(const Workspace& ws, uint64_t idx, uint32_t nrec, bool* lost) {
   *lost = nrec > GRT_WS_SLOTS && ws.pool->last[idx] == HIT_NIL;
   return *lost ? GRT_WS_SLOTS : nrec;
 }
@@ -2387,11 +2480,13 @@ GDEV uint32_t rec_read(const Workspace& ws, const RecRef& r, double* p, double* 
 // Workspace slots come back as a mask; pool records get their jobs appended here.
 template <int G>
 GDEV uint32_t march_slots(const DevScene& S, const Workspace& ws, uint64_t idx) {
-  const uint64_t n = ws.n;
-  if (ws.status[idx] != GRT_OK) return 0u;
-  RayConst rc{ws.rc[idx], ws.rc[n + idx], ws.rc[2 * n + idx], ws.rc[3 * n + idx]};
+  const RayMeta mt = meta_get(ws, idx);
+  if (mt.status != GRT_OK) return 0u;
+  RayConst rc;
+  double y[8];
+  fin_get<G>(ws, idx, y, rc);
   bool lost;
-  const uint32_t nr = rec_count(ws, idx, &lost);
+  const uint32_t nr = rec_count(ws, idx, mt.nrec, &lost);
   uint32_t mask = 0u, pool_jobs = 0u, pos = HIT_NIL;
   for (uint32_t j = 0; j < nr; ++j) {
     const RecRef r = rec_at(ws, idx, j, &pos);
@@ -2455,17 +2550,20 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(ws.pool->count + 1, *ws.pool->count);
   if (idx >= n_live) return;
-  int status = ws.status[idx];
-  int stop = ws.stop[idx];
-  uint32_t steps = ws.steps[idx];
+  const RayMeta mt = meta_get(ws, idx);
+  int status = mt.status;
+  const int stop = mt.stop;
+  const uint32_t steps = mt.steps;
   const XYZA fail{0.0, 0.0, 0.0, 1.0};
   if (status != GRT_OK) {  // integrate error: reference default pixel (raytracer.rs:204-210)
     write_out(out, idx, fail, GRT_CLASS_ESCAPED, status, stop, steps, 0u);
     return;
   }
-  RayConst rc{ws.rc[idx], ws.rc[n + idx], ws.rc[2 * n + idx], ws.rc[3 * n + idx]};
+  RayConst rc;
+  double y[8];
+  fin_get<G>(ws, idx, y, rc);
   bool lost;
-  const uint32_t nr = rec_count(ws, idx, &lost);
+  const uint32_t nr = rec_count(ws, idx, mt.nrec, &lost);
   // window-nearest hits: the first ones in registers, the later ones (pool records of
   // rays with more than GRT_WS_SLOTS candidates) next to their record, linked backwards
   XYZA hits[GRT_WS_SLOTS];
@@ -2515,9 +2613,6 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
   if (stop == GRT_STOP_HORIZON || stop == GRT_STOP_CLOSED_ORBIT) {
     result = blend(result, XYZA{0.0, 0.0, 0.0, 1.0});
   } else if (stop == GRT_STOP_CELESTIAL) {
-    double y[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) y[k] = ws.y[k * n + idx];
     double th, ph;  // get_as_spherical (point.rs:172-188)
     double st = 0.0, ct = 0.0;
     if constexpr (G == GRT_GEOM_SCHWARZSCHILD || G == GRT_GEOM_KERR_BL || G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {
