@@ -494,8 +494,8 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   const uint32_t tiles_x = wl.tiles_x, tiles_y = (uint32_t)(wl.n_items / 64 / wl.tiles_x);
   const uint64_t n = (uint64_t)tiles_x * tiles_y;
   size_t temp_bytes = 0;
-  HIP_TRY(grt::launch_tile_order(nullptr, tiles_x, tiles_y, nullptr, nullptr, nullptr, nullptr, nullptr, &temp_bytes,
-                                 stream));
+  HIP_TRY(grt::launch_tile_order(nullptr, tiles_x, tiles_y, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 &temp_bytes, stream));
   const uint64_t need = 5 * ((n * 4 + 255) & ~255ull) + temp_bytes + 256;
   if (n > dc.sched_tiles || !dc.sched_mem) {
     if (dc.sched_mem) {
@@ -520,8 +520,9 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   uint32_t* idx = (uint32_t*)take(n * 4);
   uint32_t* ord = (uint32_t*)take(n * 4);
   void* temp = take(temp_bytes);
-  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, probe_cap(s), probe, stream));
-  HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, keys, keys_sorted, idx, ord, temp, &temp_bytes, stream));
+  const uint32_t cap = probe_cap(s);
+  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, cap, probe, stream));
+  HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, cap, keys, keys_sorted, idx, ord, temp, &temp_bytes, stream));
   *order = ord;
   return 0;
 }

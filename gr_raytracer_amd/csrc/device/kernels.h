@@ -25,9 +25,10 @@ constexpr int TAIL_RAYS_PER_BLOCK = 256 / 4;
 // Work-order probe: steps of one ray per 8x8 tile of `wl` (rectangle mode), capped.
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,
                         uint32_t* d_steps, hipStream_t stream);
-// Tile queue order from the probe counts (schedule.hip): 3x3-dilated counts, sorted
-// descending (stable).  `temp` / `temp_bytes`: scratch, query with temp == NULL.
-hipError_t launch_tile_order(const uint32_t* d_probe, uint32_t tiles_x, uint32_t tiles_y, uint32_t* d_keys,
+// Tile queue order from the probe keys (schedule.hip): 3x3-dilated keys (edge tiles of a
+// region of probes that reached `cap` boosted), sorted descending (stable).  `temp` /
+// `temp_bytes`: scratch, query with temp == NULL.
+hipError_t launch_tile_order(const uint32_t* d_probe, uint32_t tiles_x, uint32_t tiles_y, uint32_t cap, uint32_t* d_keys,
                              uint32_t* d_keys_sorted, uint32_t* d_idx, uint32_t* d_order, void* temp,
                              size_t* temp_bytes, hipStream_t stream);
 
