@@ -1654,9 +1654,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   int retries = 0;
   uint32_t nrec = 0;
   RayConst rc;
-  // Counters of the wave, kept in scalar registers: each site adds the number of lanes that
-  // reach it (the exec mask's population), so no VGPR carries them through the RHS
-  uint64_t w_acc = 0, w_att = 0;
+  // per-lane counters in 32 bits (one VGPR each): a lane integrates far fewer than 2^32
+  // steps in one launch (C4 whole frame: ~5e6 per lane)
+  uint32_t n_acc = 0, n_att = 0;
   uint64_t w_rays = 0;  // rays started by this wave: counted in wave-uniform control flow (an SGPR)
 #if GRT_RAY_TIMES
   uint32_t ray_att = 0;
@@ -1819,7 +1819,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       err_sq = (UNIT_H_COPY && __ballot(active && h_cur != 1.0) == 0)
                    ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
                    : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
-      w_att += __popcll(__ballot(1));
+      n_att++;
 #if GRT_RAY_TIMES
       ray_att++;
 #endif
@@ -1830,7 +1830,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         if (__ballot(!quick_step_ok<G>(S, err_sq, y, yn, i + 1)) == 0) {
           h = rclamp(h_cur * H_GROWTH, H_MIN, H_MAX);
           i++;
-          w_acc += __popcll(__ballot(1));
+          n_acc++;
           c_valid = false;
 #pragma unroll
           for (int k = 0; k < 8; ++k) y[k] = yn[k];
@@ -1856,7 +1856,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     // ---------------- accepted step i (integrator.rs:100-162) --------------------
     h = h_next;
     i++;
-    w_acc += __popcll(__ballot(1));
+    n_acc++;
     window_pass<G, VOL>(S, ws, rc, idx, y, yn, c, c_valid, i, nrec, true);
 #pragma unroll
     for (int k = 0; k < 8; ++k) y[k] = yn[k];
@@ -1873,7 +1873,13 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     h_cur = rclamp(h, H_MIN, H_MAX);
   }
 
-  // one atomic per counter and wave
+  // per-wave reduction of the counters, one atomic per wave
+  uint64_t w_acc = n_acc, w_att = n_att;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    w_acc += __shfl_down(w_acc, off);
+    w_att += __shfl_down(w_att, off);
+  }
   if (lane == 0) {
     atomicAdd(stats + 0, (unsigned long long)w_acc);
     atomicAdd(stats + 1, (unsigned long long)w_att);
