@@ -166,7 +166,7 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   // volumetric scenes: rc grows to 6 doubles; chord directions, raymarched colours, jobs
   // final-state record (64 B), meta record (16 B), pool list ends (8 B), candidate slots;
   // volumetric scenes: the ray constants (48 B), chord directions, raymarched colours, jobs
-  const uint64_t per_ray = 64 + 16 + 8 + M * (4 + 1 + 4 * 8 + 3 * 8) + (vol ? 6 * 8 + M * (3 * 8 + 4 * 8 + 8) : 0);
+  const uint64_t per_ray = 64 + 16 + 8 + M * 64 + (vol ? 6 * 8 + M * (3 * 8 + 4 * 8 + 8) : 0);
   // volumetric scenes: the raymarch job list also holds one job per pool record
   const uint64_t jobs_extra = vol ? dc.pool_cap : 0;
   if (n > dc.ws_cap || (vol && !dc.ws_vol) || jobs_extra > dc.ws_jobs_pool) {
@@ -197,12 +197,9 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   ws->fin = (double*)take(64 * cap);
   ws->meta = (uint32_t*)take(16 * cap);
   ws->rc = vol ? (double*)take(6 * 8 * cap) : nullptr;
-  ws->rec_p = (double*)take(4 * M * 8 * cap);
-  ws->rec_pt = (double*)take(3 * M * 8 * cap);
-  ws->rec_win = (uint32_t*)take(M * 4 * cap);
+  ws->rec = (grt::CandRec*)take(M * 64 * cap);
   dc.ws_head = (uint32_t*)take(4 * cap);
   dc.ws_last = (uint32_t*)take(4 * cap);
-  ws->rec_obj = (uint8_t*)take(M * cap);
   ws->rec_dir = ws->vcol = nullptr;
   ws->jobs = nullptr;
   ws->march = dc.d_march;

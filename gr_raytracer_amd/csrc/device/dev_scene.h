@@ -155,6 +155,16 @@ struct HitPool {
                              //     HIT_NIL once one was lost
 };
 
+// A window candidate in a workspace slot: 64 B, written whole (four 16-B stores) by the
+// lane that records it.
+struct CandRec {
+  double p[4];   // momentum lerped to the hit (objects.rs:27-44)
+  double pt[3];  // hit point (sphere-local for spheres)
+  uint32_t win;  // window (accepted-step) index
+  uint32_t obj;  // object index
+};
+static_assert(sizeof(CandRec) == 64, "candidate record: one 64-B line");
+
 // Hand-off from the integrate kernel to the shade kernel, n = number of output slots of
 // the launch.  Per ray, written once by the lane that ends it, as two records of whole
 // 16-B stores (a 64-B line and a quarter of one, instead of one 8-B store per field into
@@ -169,10 +179,7 @@ struct Workspace {
   uint32_t* meta;     // [n][4] steps, candidates, stop | status << 8, 0
   double* rc;         // volumetric scenes only: [6][n] ray constants (observer energy, E, L_z,
                       // Q, p_t, p_phi) written at the ray's start, for the raymarch
-  uint32_t* rec_win;  // [MAX][n] window (accepted-step) index
-  uint8_t* rec_obj;   // [MAX][n] object index
-  double* rec_p;      // [4][MAX][n] momentum lerped to the hit (objects.rs:27-44)
-  double* rec_pt;     // [3][MAX][n] hit point (sphere-local for spheres)
+  CandRec* rec;       // [MAX][n] candidate records, slot j of ray i at j * n + i
   // volumetric scenes only (NULL otherwise)
   double* rec_dir;    // [3][MAX][n] chord direction y_end - y_start (volumetric candidates)
   double* vcol;       // [4][MAX][n] raymarched colour of volumetric candidate slots

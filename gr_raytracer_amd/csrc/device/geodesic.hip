@@ -58,6 +58,9 @@ namespace grt {
 #ifndef GRT_FIN_CONST_AT_START
 #define GRT_FIN_CONST_AT_START 0  // write the ray constants into the final-state record at the ray's start
 #endif
+#ifndef GRT_CART_LDS
+#define GRT_CART_LDS 1  // integrate kernels at 3 waves per SIMD keep the Cartesian cache in LDS
+#endif
 #ifndef GRT_RAY_TIMES
 #define GRT_RAY_TIMES 0  // diagnostic builds only: per-ray schedule record (tools/c4_ray_times.py)
 #endif
@@ -68,7 +71,7 @@ namespace grt {
 #define GRT_SLOW_NOINLINE 1
 #endif
 #if GRT_SLOW_NOINLINE
-#define GRT_SLOW __device__ __attribute__((noinline))
+#define GRT_SLOW __device__ __attribute__((noinline, cold))
 #else
 #define GRT_SLOW GDEV
 #endif
@@ -1524,12 +1527,11 @@ GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc
         momentum<G>(S, rc, yn, pb);
         double sw = 1.0 - t;
         const uint64_t slot = (uint64_t)nrec * n + idx;
-        ws.rec_win[slot] = (uint32_t)i;
-        ws.rec_obj[slot] = (uint8_t)k;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ws.rec_p[(uint64_t)q * GRT_WS_SLOTS * n + slot] = sw * pa[q] + t * pb[q];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) ws.rec_pt[(uint64_t)q * GRT_WS_SLOTS * n + slot] = pt[q];
+        double2* d = reinterpret_cast<double2*>(ws.rec + slot);
+        d[0] = make_double2(sw * pa[0] + t * pb[0], sw * pa[1] + t * pb[1]);
+        d[1] = make_double2(sw * pa[2] + t * pb[2], sw * pa[3] + t * pb[3]);
+        d[2] = make_double2(pt[0], pt[1]);
+        d[3] = make_double2(pt[2], __hiloint2double((int)k, (int)(uint32_t)i));
         if constexpr (VOL) {  // chord direction for the raymarch (volumetric_disc.rs:576, :589-594)
           ws.rec_dir[slot] = cn[0] - c[0];
           ws.rec_dir[(uint64_t)GRT_WS_SLOTS * n + slot] = cn[1] - c[1];
@@ -1647,7 +1649,17 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   bool q_drained = false;  // this wave has seen the tile queue drained (it stays drained)
   uint64_t idx = 0;      // output slot of the current ray
   double y[8];           // state
-  double c[3];           // Cartesian position of the last accepted step (when c_valid)
+  // Cartesian position of the last accepted step (when c_valid).  The 3-wave kernels
+  // (Schwarzschild, KerrBL, flat charts: 168 VGPRs) keep it in LDS: it is read only by
+  // the near-field window pass and the celestial test, and in registers it stays live
+  // across every RHS evaluation (values stored and read back unchanged).
+#if GRT_CART_LDS
+  __shared__ double c_lds[(G == GRT_GEOM_KERR || VOL) ? 1 : 3 * 256];
+  double c_regs[3];
+  double* const c = (G == GRT_GEOM_KERR || VOL) ? c_regs : &c_lds[3 * threadIdx.x];
+#else
+  double c[3];
+#endif
   bool c_valid = false;
   double h = 0.0, h_cur = 0.0;
   uint64_t i = 0;        // accepted step index
@@ -2450,21 +2462,25 @@ GDEV RecRef rec_at(const Workspace& ws, uint64_t idx, uint32_t j, uint32_t* pos)
   *pos = (j == GRT_WS_SLOTS) ? ws.pool->head[idx] : ws.pool->next[*pos];
   return RecRef{true, *pos};
 }
-GDEV uint32_t rec_win(const Workspace& ws, const RecRef& r) { return r.pool ? ws.pool->win[r.s] : ws.rec_win[r.s]; }
+GDEV uint32_t rec_win(const Workspace& ws, const RecRef& r) { return r.pool ? ws.pool->win[r.s] : ws.rec[r.s].win; }
 // The window of candidate j + 1 (which exists), given candidate j.
 GDEV uint32_t rec_next_win(const Workspace& ws, uint64_t idx, uint32_t j, const RecRef& r) {
-  if (j + 1 < GRT_WS_SLOTS) return ws.rec_win[r.s + ws.n];
+  if (j + 1 < GRT_WS_SLOTS) return ws.rec[r.s + ws.n].win;
   if (j + 1 == GRT_WS_SLOTS) return ws.pool->win[ws.pool->head[idx]];
   return ws.pool->win[ws.pool->next[r.s]];
 }
 GDEV uint32_t rec_read(const Workspace& ws, const RecRef& r, double* p, double* pt) {
   if (!r.pool) {
-    const uint64_t MN = (uint64_t)GRT_WS_SLOTS * ws.n;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) p[q] = ws.rec_p[q * MN + r.s];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) pt[q] = ws.rec_pt[q * MN + r.s];
-    return ws.rec_obj[r.s];
+    const double2* d = reinterpret_cast<const double2*>(ws.rec + r.s);
+    const double2 a = d[0], b = d[1], c = d[2], e = d[3];
+    p[0] = a.x;
+    p[1] = a.y;
+    p[2] = b.x;
+    p[3] = b.y;
+    pt[0] = c.x;
+    pt[1] = c.y;
+    pt[2] = e.x;
+    return (uint32_t)__double2hiint(e.y);
   }
   const uint64_t m = ws.pool->cap;
 #pragma unroll

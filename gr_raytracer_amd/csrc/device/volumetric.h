@@ -390,8 +390,8 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
             idx = job >> 8;
             const uint32_t j = (uint32_t)(job & 255u);
             slot = (uint64_t)j * n + idx;
-            k = ws.rec_obj[slot];
-            ro = V3{ws.rec_pt[slot], ws.rec_pt[MN + slot], ws.rec_pt[2 * MN + slot]};
+            k = ws.rec[slot].obj;
+            ro = V3{ws.rec[slot].pt[0], ws.rec[slot].pt[1], ws.rec[slot].pt[2]};
             dir = V3{ws.rec_dir[slot], ws.rec_dir[MN + slot], ws.rec_dir[2 * MN + slot]};
           } else {  // a candidate past the workspace slots (HitPool record)
             idx = (job & ~JOB_POOL) >> 31;
