@@ -308,6 +308,10 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     int ex = 0;
     std::frexp(d.radius, &ex);
     ds.div_share = (std::fpclassify(d.radius) == FP_NORMAL && ex > -500 && ex < 500) ? 1 : 0;
+    int ea = 0;
+    std::frexp(d.a, &ea);
+    const bool a_ok = d.geometry != GRT_GEOM_KERR_BL || (std::fpclassify(d.a) == FP_NORMAL && ea > -50 && ea < 50);
+    ds.div_fast = (std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -50 && ex < 50 && a_ok) ? 1 : 0;
   }
   {  // exact controller shortcuts (geodesic.hip step_control); off unless epsilon is a moderate normal
     int ex = 0;
@@ -766,6 +770,24 @@ int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n,
   return 0;
 }
 #endif
+
+// Test hook (not in grt_api.h): the range-checked division of the speculative attempt
+// (geodesic.hip div_inrange) against the compiler's f64 division on n random operand
+// pairs; *mismatches = pairs whose bits differ (0 expected).
+int grt_debug_div_check(int device, uint64_t n, uint64_t seed, uint64_t* mismatches) {
+  if (!mismatches || n == 0 || n > (1ull << 32)) return fail(-EINVAL, "div check: 1 <= n <= 2^32");
+  HIP_TRY(hipSetDevice(device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMalloc(&d, 8));
+  hipError_t e = hipMemset(d, 0, 8);
+  if (e == hipSuccess) e = grt::launch_div_check(n, seed, d, nullptr);
+  unsigned long long h = 0;
+  if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  HIP_TRY(e);
+  *mismatches = h;
+  return 0;
+}
 
 int grt_set_two_ended(int on) {
   if (on != 0 && on != 1) return fail(-EINVAL, "two-ended queue: 0 or 1");

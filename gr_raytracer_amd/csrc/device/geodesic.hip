@@ -49,6 +49,9 @@ namespace grt {
 #ifndef GRT_SINCOS_B
 #define GRT_SINCOS_B 1  // Schwarzschild / KerrBL RHS: wave-uniform straight-line sincos (region B)
 #endif
+#ifndef GRT_FAST_DIV
+#define GRT_FAST_DIV 1  // Schwarzschild / KerrBL region-B RHS: divisions without range steps when the operands allow
+#endif
 #ifndef GRT_QUICK_STEP
 #define GRT_QUICK_STEP 1  // Schwarzschild: the far-field accepted step as one straight-line block
 #endif
@@ -57,9 +60,6 @@ namespace grt {
 #endif
 #ifndef GRT_FIN_CONST_AT_START
 #define GRT_FIN_CONST_AT_START 0  // write the ray constants into the final-state record at the ray's start
-#endif
-#ifndef GRT_CART_LDS
-#define GRT_CART_LDS 1  // integrate kernels at 3 waves per SIMD keep the Cartesian cache in LDS
 #endif
 #ifndef GRT_RAY_TIMES
 #define GRT_RAY_TIMES 0  // diagnostic builds only: per-ray schedule record (tools/c4_ray_times.py)
@@ -140,6 +140,68 @@ GDEV void div2_same_den(double x1, double x2, double y, double* q1, double* q2) 
   const double n2 = __builtin_amdgcn_div_scale(x2, y, true, &f2);
   const double m2 = n2 * fma3;
   *q2 = __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(__builtin_fma(-ds0, m2, n2), fma3, m2, f2), y, x2);
+}
+
+// x / y as that same expansion without its range steps, for operands the caller has
+// shown to be normals with |x|, |y|, |x / y| all within 2^-600 .. 2^600: there
+// v_div_scale returns its operand unchanged and raises no flag (the exponent gap is
+// < 768, neither 1 / y nor x / y is denormal, exp(x) > 53), so v_div_fmas is a plain
+// fma, and v_div_fixup, which only rewrites NaN / infinity / zero / overflow / underflow
+// cases, passes the quotient through.
+// The same instructions on the same values, hence x / y's bits (checked on the device
+// against the compiler's division, tests/test_gpu_parity.py::test_division_in_range).
+// 8 VALU instead of 11; div2_inrange shares 1 / y: 11 instead of 16.
+GDEV double div_inrange(double x, double y) {
+  const double rcp = __builtin_amdgcn_rcp(y);
+  const double fma0 = __builtin_fma(-y, rcp, 1.0);
+  const double fma1 = __builtin_fma(rcp, fma0, rcp);
+  const double fma2 = __builtin_fma(-y, fma1, 1.0);
+  const double fma3 = __builtin_fma(fma1, fma2, fma1);
+  const double m = x * fma3;
+  return __builtin_fma(__builtin_fma(-y, m, x), fma3, m);
+}
+GDEV void div2_inrange(double x1, double x2, double y, double* q1, double* q2) {
+  const double rcp = __builtin_amdgcn_rcp(y);
+  const double fma0 = __builtin_fma(-y, rcp, 1.0);
+  const double fma1 = __builtin_fma(rcp, fma0, rcp);
+  const double fma2 = __builtin_fma(-y, fma1, 1.0);
+  const double fma3 = __builtin_fma(fma1, fma2, fma1);
+  const double m1 = x1 * fma3;
+  *q1 = __builtin_fma(__builtin_fma(-y, m1, x1), fma3, m1);
+  const double m2 = x2 * fma3;
+  *q2 = __builtin_fma(__builtin_fma(-y, m2, x2), fma3, m2);
+}
+// |x| in (2^-300, 2^300), NaN excluded: two compares with the abs modifier
+GDEV bool in_div_range(double x) { return fabs(x) > 0x1p-300 && fabs(x) < 0x1p300; }
+
+// Device check of div_inrange / div2_inrange against the compiler's division: n random
+// pairs (splitmix64) with |x|, |y| in 2^-300 .. 2^300, both signs; counts[0] = pairs
+// whose bits differ.
+__global__ void div_check_kernel(uint64_t n, uint64_t seed, unsigned long long* counts) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  auto mix = [](uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+  };
+  const uint64_t u = mix(seed ^ (i * 2 + 1)), v = mix(seed ^ (i * 2 + 2));
+  // exponents: a quarter of the pairs near 1 (the common case), the rest spread
+  const int ex = (u & 3) ? (int)((u >> 52) % 601) - 300 : (int)((u >> 52) % 9) - 4;
+  const int ey = (v & 3) ? (int)((v >> 52) % 601) - 300 : (int)((v >> 52) % 9) - 4;
+  double x = __longlong_as_double((long long)((u & 0x800fffffffffffffull) | ((uint64_t)(1023 + ex) << 52)));
+  double y = __longlong_as_double((long long)((v & 0x800fffffffffffffull) | ((uint64_t)(1023 + ey) << 52)));
+  const double x2 = 2.0 * x;
+  volatile double vx = x, vy = y, vx2 = x2;  // keep the reference divisions as divisions
+  const double ref1 = vx / vy, ref2 = vx2 / vy;
+  double q1, q2;
+  div2_inrange(x, x2, y, &q1, &q2);
+  const double q0 = div_inrange(x, y);
+  const bool bad = __double_as_longlong(q0) != __double_as_longlong(ref1) ||
+                   __double_as_longlong(q1) != __double_as_longlong(ref1) ||
+                   __double_as_longlong(q2) != __double_as_longlong(ref2);
+  if (bad) atomicAdd(counts, 1ull);
 }
 
 constexpr double PI = 3.14159265358979323846;
@@ -350,26 +412,42 @@ GDEV void metric_bl(double r_s, double a, double r, double sin_t, double cos_t, 
 // dependency chains (the divisions) interleave with the sincos polynomial; fast = true
 // there (the caller passes fast_ok = whether body may then take its fast form).  The same
 // bits as rsincos in every case (tests/test_glibc_math.py).
+// div_ok (per lane): the body's divisions may drop their range steps (div_inrange) in the
+// region-B cases; body's fourth argument says so at compile time (std::true_type), so
+// each form is one basic block from the sincos through the body.
 template <class F>
-GDEV void with_sincos(double theta, bool fast_ok, F&& body) {
+GDEV void with_sincos(double theta, bool fast_ok, F&& body, bool div_ok = false) {
 #if GRT_SINCOS_B
   if (fast_ok) {
     double st, ct;
-    if (__ballot(!glibc::sincos_b_table_ok(theta)) == 0) {
+    const bool tab = glibc::sincos_b_table_ok(theta), tay = glibc::sincos_b_taylor_ok(theta);
+#if GRT_FAST_DIV
+    if (__ballot(!(tab & div_ok)) == 0) {
       glibc::sincos_b_table(theta, &st, &ct);
-      body(st, ct, true);
+      body(st, ct, true, std::true_type{});
       return;
     }
-    if (__ballot(!glibc::sincos_b_taylor_ok(theta)) == 0) {
+    if (__ballot(!(tay & div_ok)) == 0) {
       glibc::sincos_b_taylor(theta, &st, &ct);
-      body(st, ct, true);
+      body(st, ct, true, std::true_type{});
+      return;
+    }
+#endif
+    if (__ballot(!tab) == 0) {
+      glibc::sincos_b_table(theta, &st, &ct);
+      body(st, ct, true, std::false_type{});
+      return;
+    }
+    if (__ballot(!tay) == 0) {
+      glibc::sincos_b_taylor(theta, &st, &ct);
+      body(st, ct, true, std::false_type{});
       return;
     }
   }
 #endif
   double st, ct;
   rsincos(theta, &st, &ct);
-  body(st, ct, false);
+  body(st, ct, false, std::false_type{});
 }
 
 // ---- the ODE right-hand sides ----
@@ -379,7 +457,24 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     double radius = S.radius;
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
-    auto body = [&](double st, double ct, bool fast) {
+    auto body = [&](double st, double ct, bool fast, auto fdiv) {
+      if constexpr (decltype(fdiv)::value) {
+        double radius_over_r, two_over_r;
+        div2_inrange(radius, 2.0, r, &radius_over_r, &two_over_r);
+        double a = 1.0 - radius_over_r;
+        double a_prime = div_inrange(radius, r * r);
+        double aprime_over_a = div_inrange(a_prime, a);
+        o[0] = v_t;
+        o[1] = v_r;
+        o[2] = v_theta;
+        o[3] = v_phi;
+        o[4] = -(aprime_over_a)*v_t * v_r;
+        o[5] = -0.5 * a * a_prime * v_t * v_t + 0.5 * (aprime_over_a)*v_r * v_r +
+               a * r * (v_theta * v_theta + v_phi * v_phi * st * st);
+        o[6] = -(two_over_r)*v_r * v_theta + st * ct * v_phi * v_phi;
+        o[7] = -(two_over_r)*v_phi * v_r - div_inrange(2.0 * ct, st) * v_theta * v_phi;
+        return;
+      }
       double radius_over_r, two_over_r;
 #if GRT_SHARED_DIV
       if (fast || S.div_share) {
@@ -403,8 +498,14 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
       o[6] = -(two_over_r)*v_r * v_theta + st * ct * v_phi * v_phi;
       o[7] = -(two_over_r)*v_phi * v_r - 2.0 * ct / st * v_theta * v_phi;
     };
-    // fast form: the shared reciprocal, decided with the wave-uniform case (S.div_share)
-    with_sincos(theta, S.div_share, body);
+    // fast form: the shared reciprocal, decided with the wave-uniform case (S.div_share).
+    // Divisions without range steps (div_inrange) in region B: there sin theta >= 0.75 and
+    // 2^-55 < |cos theta| < 0.66, and with S.div_fast (0 < radius within 2^+-50),
+    // 2^-100 < |r| < 2^100 and |r - radius| > 2^-40 radius (so |a| > 2^-42), every operand
+    // and quotient of the five divisions is within 2^+-600.
+    const bool div_ok = S.div_fast && (fabs(r) > 0x1p-100) & (fabs(r) < 0x1p100) &
+                        (fabs(r - radius) > radius * 0x1p-40);
+    with_sincos(theta, S.div_share, body, div_ok);
   } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:48-70
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
@@ -421,11 +522,26 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
   } else if constexpr (G == GRT_GEOM_KERR_BL) {  // kerr_bl.rs:141-174
     double radius = S.radius, a = S.a, e = rc.e, l_z = rc.lz, q = rc.q;
     double r = y[1], theta = y[2];
-    with_sincos(theta, true, [&](double st, double ct, bool) {
-      double del = bl_delta(r, radius, a);
+    const double del = bl_delta(r, radius, a);
+    auto body = [&](double st, double ct, bool, auto fdiv) {
       double r2a2 = r * r + a * a;
       double p_r = r2a2 * e - a * l_z;
       double sin2 = st * st;
+      if constexpr (decltype(fdiv)::value) {
+        double r2a2_del, a_del;
+        div2_inrange(r2a2, a, del, &r2a2_del, &a_del);
+        o[0] = r2a2_del * p_r + a * (l_z - a * e * sin2);
+        o[1] = y[4];
+        o[2] = y[5];
+        o[3] = a_del * p_r + div_inrange(l_z, sin2) - a * e;
+        double le = l_z - a * e;
+        double carter = le * le + q;
+        o[4] = (4.0 * r * e * p_r - (2.0 * r - radius) * carter) / 2.0;
+        o[5] = (-2.0 * a * a * e * e * ct * st + div_inrange(2.0 * l_z * l_z * ct, st * (st * st))) / 2.0;
+        o[6] = 0.0;
+        o[7] = 0.0;
+        return;
+      }
       o[0] = r2a2 / del * p_r + a * (l_z - a * e * sin2);
       o[1] = y[4];
       o[2] = y[5];
@@ -436,7 +552,14 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
       o[5] = (-2.0 * a * a * e * e * ct * st + 2.0 * l_z * l_z * ct / (st * (st * st))) / 2.0;
       o[6] = 0.0;
       o[7] = 0.0;
-    });
+    };
+    // Divisions without range steps (div_inrange) in region B: there sin theta >= 0.75 and
+    // 2^-55 < |cos theta| < 0.66, and with S.div_fast (radius, |a| within 2^+-50),
+    // 2^-200 < |l_z| < 2^100, |r| < 2^100 and del within 2^+-300, every operand and
+    // quotient of the four divisions is within 2^+-600.
+    const bool div_ok = S.div_fast && (fabs(r) < 0x1p100) & in_div_range(del) & (fabs(l_z) > 0x1p-200) &
+                        (fabs(l_z) < 0x1p100);
+    with_sincos(theta, true, body, div_ok);
   } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:200-241
     double radius = S.radius, a = S.a;
     double x = y[1], yy = y[2], z = y[3];
@@ -1649,17 +1772,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   bool q_drained = false;  // this wave has seen the tile queue drained (it stays drained)
   uint64_t idx = 0;      // output slot of the current ray
   double y[8];           // state
-  // Cartesian position of the last accepted step (when c_valid).  The 3-wave kernels
-  // (Schwarzschild, KerrBL, flat charts: 168 VGPRs) keep it in LDS: it is read only by
-  // the near-field window pass and the celestial test, and in registers it stays live
-  // across every RHS evaluation (values stored and read back unchanged).
-#if GRT_CART_LDS
-  __shared__ double c_lds[(G == GRT_GEOM_KERR || VOL) ? 1 : 3 * 256];
-  double c_regs[3];
-  double* const c = (G == GRT_GEOM_KERR || VOL) ? c_regs : &c_lds[3 * threadIdx.x];
-#else
-  double c[3];
-#endif
+  double c[3];           // Cartesian position of the last accepted step (when c_valid)
   bool c_valid = false;
   double h = 0.0, h_cur = 0.0;
   uint64_t i = 0;        // accepted step index
@@ -2069,6 +2182,11 @@ __global__ void __launch_bounds__(64) trajectory_kernel(const DevScene* __restri
   tl.n_steps[r] = count;
   tl.stop[r] = (uint8_t)stop;
   tl.status[r] = (uint8_t)status;
+}
+
+hipError_t launch_div_check(uint64_t n, uint64_t seed, unsigned long long* d_counts, hipStream_t stream) {
+  hipLaunchKernelGGL(div_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, seed, d_counts);
+  return hipGetLastError();
 }
 
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream) {

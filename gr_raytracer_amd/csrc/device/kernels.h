@@ -46,6 +46,8 @@ struct TrajectoryList {
   uint8_t* stop;
   uint8_t* status;
 };
+// test hook: div_inrange / div2_inrange against the compiler's division on n random pairs
+hipError_t launch_div_check(uint64_t n, uint64_t seed, unsigned long long* d_counts, hipStream_t stream);
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
 
 // Invariant monitors of the n = rows x cols rays of a rectangle (health_kernel):

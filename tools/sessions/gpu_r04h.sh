@@ -1,0 +1,19 @@
+#!/bin/bash
+# r04h: candidate records (64 B) + LDS Cartesian cache: C2 / C3 A/B against the previous
+# commit (md5 and time), C4 shard 2, the whole GPU suite, then PMC passes (C2, C3, C4 2/8)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+( while sleep 60; do echo "[heartbeat] $(date +%T)" >&2; done ) &
+HB=$!
+trap "kill $HB" EXIT
+OUT=gpurun_out/r04h; mkdir -p $OUT
+GRT_LIB_ALLOW_MISSING=1 timeout -k 10 300 python3 tools/time_variants.py base new base new >> $OUT/c2c3_ab.jsonl 2> $OUT/ab.err || { tail $OUT/ab.err >&2; exit 1; }
+cat $OUT/c2c3_ab.jsonl >&2
+timeout -k 10 200 python3 tools/c4_shard_time.py 8 2 >> $OUT/c4_shard2.jsonl 2> $OUT/c4.err || { tail -20 $OUT/c4.err >&2; exit 1; }
+cut -c1-300 $OUT/c4_shard2.jsonl >&2
+timeout -k 10 700 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log >&2; exit 1; }
+tail -3 $OUT/pytest_gpu.log >&2
+MEMPASS=1 bash tools/run_pmc.sh r04h_c2 c2 >&2 || exit 1
+MEMPASS=1 bash tools/run_pmc.sh r04h_c3 c3 >&2 || exit 1
+bash tools/run_pmc.sh r04h_c4 c4 >&2 || exit 1
