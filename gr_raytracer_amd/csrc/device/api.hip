@@ -163,8 +163,7 @@ grt::HitPool pool_view(const DeviceCopy& dc) {
 int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   const uint64_t M = GRT_WS_SLOTS;
   const bool vol = dc.vol;
-  // volumetric scenes: rc grows to 6 doubles; chord directions, raymarched colours, jobs
-  // final-state record (64 B), meta record (16 B), pool list ends (8 B), candidate slots;
+  // ray record (64 B), KerrBL's meta record (16 B), pool list ends (8 B), candidate slots;
   // volumetric scenes: the ray constants (48 B), chord directions, raymarched colours, jobs
   const uint64_t per_ray = 64 + 16 + 8 + M * 64 + (vol ? 6 * 8 + M * (3 * 8 + 4 * 8 + 8) : 0);
   // volumetric scenes: the raymarch job list also holds one job per pool record
@@ -196,6 +195,7 @@ int ensure_workspace(DeviceCopy& dc, uint64_t n, grt::Workspace* ws) {
   ws->n = n;
   ws->fin = (double*)take(64 * cap);
   ws->meta = (uint32_t*)take(16 * cap);
+  ws->steps = nullptr;  // launch_trace points it at Outputs::steps
   ws->rc = vol ? (double*)take(6 * 8 * cap) : nullptr;
   ws->rec = (grt::CandRec*)take(M * 64 * cap);
   dc.ws_head = (uint32_t*)take(4 * cap);

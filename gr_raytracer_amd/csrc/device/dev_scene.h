@@ -166,17 +166,17 @@ struct CandRec {
 static_assert(sizeof(CandRec) == 64, "candidate record: one 64-B line");
 
 // Hand-off from the integrate kernel to the shade kernel, n = number of output slots of
-// the launch.  Per ray, written once by the lane that ends it, as two records of whole
-// 16-B stores (a 64-B line and a quarter of one, instead of one 8-B store per field into
-// a structure-of-arrays slot: rays end one by one in probe order, so those lines were
-// written back part-filled): the final state and the constants the shade needs (fin,
-// layout in geodesic.hip fin_put), and the step count, candidate count, stop reason and
-// status (meta).  The window candidates: the first GRT_WS_SLOTS in slots (slot-major:
-// slot k of ray i at k*n + i), the rest in the hit pool.
+// the launch.  Per ray, written once by the lane that ends it, as one 64-B record of
+// whole 16-B stores (not one 8-B store per field into structure-of-arrays slots, nor a
+// second small record: rays end one by one in probe order, so lines shared by several
+// rays were written back part-filled, once per ray): the final state, the constants the
+// shade needs, the candidate count, stop reason and status (fin; layout and KerrBL's
+// 16-B meta record in geodesic.hip fin_put).  The window candidates: the first GRT_WS_SLOTS in slots (slot-major: slot k
+// of ray i at k*n + i, one 64-B record each), the rest in the hit pool.
 struct Workspace {
   uint64_t n;
-  double* fin;        // [n][8] final-state record (64 B, 64-B aligned)
-  uint32_t* meta;     // [n][4] steps, candidates, stop | status << 8, 0
+  double* fin;        // [n][8] ray record (64 B, 64-B aligned)
+  uint32_t* meta;     // KerrBL: [n][4] steps, candidates, stop | status << 8, 0
   double* rc;         // volumetric scenes only: [6][n] ray constants (observer energy, E, L_z,
                       // Q, p_t, p_phi) written at the ray's start, for the raymarch
   CandRec* rec;       // [MAX][n] candidate records, slot j of ray i at j * n + i
@@ -191,6 +191,7 @@ struct Workspace {
   // n stays the SoA stride
   const unsigned long long* n_live;
   const HitPool* pool;  // device memory
+  uint32_t* steps;      // optional per-pixel step counts (Outputs::steps), written at the ray's end
 };
 constexpr uint64_t JOB_POOL = 1ull << 63;
 

@@ -52,14 +52,17 @@ namespace grt {
 #ifndef GRT_FAST_DIV
 #define GRT_FAST_DIV 1  // Schwarzschild / KerrBL region-B RHS: divisions without range steps when the operands allow
 #endif
+#ifndef GRT_FAST_DIV_BL
+// KerrBL too: C3 is no faster with it (165-172 ms either way), but its 3-wave kernel's
+// spills land elsewhere: 1.71 GB written per frame with it, 20.9 GB without
+// (profiles/r04n_c3_pmc.json, r04o_c3_pmc.json)
+#define GRT_FAST_DIV_BL 1
+#endif
 #ifndef GRT_QUICK_STEP
 #define GRT_QUICK_STEP 1  // Schwarzschild: the far-field accepted step as one straight-line block
 #endif
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
-#endif
-#ifndef GRT_FIN_CONST_AT_START
-#define GRT_FIN_CONST_AT_START 0  // write the ray constants into the final-state record at the ray's start
 #endif
 #ifndef GRT_RAY_TIMES
 #define GRT_RAY_TIMES 0  // diagnostic builds only: per-ray schedule record (tools/c4_ray_times.py)
@@ -415,24 +418,24 @@ GDEV void metric_bl(double r_s, double a, double r, double sin_t, double cos_t, 
 // div_ok (per lane): the body's divisions may drop their range steps (div_inrange) in the
 // region-B cases; body's fourth argument says so at compile time (std::true_type), so
 // each form is one basic block from the sincos through the body.
-template <class F>
+template <bool FDIV = false, class F>
 GDEV void with_sincos(double theta, bool fast_ok, F&& body, bool div_ok = false) {
 #if GRT_SINCOS_B
   if (fast_ok) {
     double st, ct;
     const bool tab = glibc::sincos_b_table_ok(theta), tay = glibc::sincos_b_taylor_ok(theta);
-#if GRT_FAST_DIV
-    if (__ballot(!(tab & div_ok)) == 0) {
-      glibc::sincos_b_table(theta, &st, &ct);
-      body(st, ct, true, std::true_type{});
-      return;
+    if constexpr (FDIV) {
+      if (__ballot(!(tab & div_ok)) == 0) {
+        glibc::sincos_b_table(theta, &st, &ct);
+        body(st, ct, true, std::true_type{});
+        return;
+      }
+      if (__ballot(!(tay & div_ok)) == 0) {
+        glibc::sincos_b_taylor(theta, &st, &ct);
+        body(st, ct, true, std::true_type{});
+        return;
+      }
     }
-    if (__ballot(!(tay & div_ok)) == 0) {
-      glibc::sincos_b_taylor(theta, &st, &ct);
-      body(st, ct, true, std::true_type{});
-      return;
-    }
-#endif
     if (__ballot(!tab) == 0) {
       glibc::sincos_b_table(theta, &st, &ct);
       body(st, ct, true, std::false_type{});
@@ -505,7 +508,7 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     // and quotient of the five divisions is within 2^+-600.
     const bool div_ok = S.div_fast && (fabs(r) > 0x1p-100) & (fabs(r) < 0x1p100) &
                         (fabs(r - radius) > radius * 0x1p-40);
-    with_sincos(theta, S.div_share, body, div_ok);
+    with_sincos<GRT_FAST_DIV>(theta, S.div_share, body, div_ok);
   } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:48-70
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
@@ -559,7 +562,7 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     // quotient of the four divisions is within 2^+-600.
     const bool div_ok = S.div_fast && (fabs(r) < 0x1p100) & in_div_range(del) & (fabs(l_z) > 0x1p-200) &
                         (fabs(l_z) < 0x1p100);
-    with_sincos(theta, true, body, div_ok);
+    with_sincos<GRT_FAST_DIV_BL>(theta, true, body, div_ok);
   } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:200-241
     double radius = S.radius, a = S.a;
     double x = y[1], yy = y[2], z = y[3];
@@ -1264,6 +1267,22 @@ GDEV void init_state(const DevScene& S, const double* pos, double st, double ct,
   }
 }
 
+// The image coordinates of the ray in output slot idx of a work list: an offset list's
+// jittered pixel (get_ray_for_offset, camera.rs:247-254), or the pixel of a rectangle /
+// row-band shard (local row idx / cols, mapped to its frame row).
+GDEV void ray_pixel(const WorkList& wl, uint64_t idx, double* row, double* col) {
+  if (wl.pixel_index) {
+    const uint32_t pix = wl.pixel_index[idx];
+    const double r = (double)(wl.row0 + pix / wl.cols), cc = (double)(wl.col0 + pix % wl.cols);
+    *row = r + (wl.dy[idx] - 0.5);
+    *col = cc + (wl.dx[idx] - 0.5);
+  } else {
+    const uint32_t r = (uint32_t)(idx / wl.cols), cc = (uint32_t)(idx % wl.cols);
+    *row = (double)(wl.row0 + shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, r));
+    *col = (double)(wl.col0 + cc);
+  }
+}
+
 // Create a camera ray's state (camera.rs:234-254 + init_state); also the observer
 // energy the redshift needs (redshift.rs:40-43).
 template <int G, bool FREQ = false>
@@ -1272,7 +1291,7 @@ GDEV void init_ray(const DevScene& S, double row, double col, double* y, RayCons
   double p[4];
   camera_momentum(cam, row, col, p);
   init_state<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, p, y, rc);
-  rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
+  rc.obs = inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);  // = observer_energy
   rc.pt = 0.0;
   rc.pphi = 0.0;
   if constexpr (FREQ) {  // get_ray_frequency_data: <e_t, p> and <axial Killing vector, p>
@@ -1488,13 +1507,37 @@ hipError_t set_ray_times(unsigned long long* p) { return hipMemcpyToSymbol(HIP_S
 #define RAY_TIME(n, idx, k, v) ((void)0)
 #endif
 
-// The final-state record of a ray (Workspace::fin, 8 doubles): what the shade kernel reads
-// of the state and the ray constants.  KerrBL: r, theta, phi, v_r, v_theta, observer
-// energy, E, L_z (y[6], y[7] are identically 0, Q only drives the RHS); the other charts:
-// y[1..7] and the observer energy (y[0] is not read; Kerr-Schild's momentum needs none
-// of E, L_z, Q).
+// The observer energy of the camera ray in output slot idx (init_ray's rc.obs, recomputed
+// by the shade kernels instead of stored).
 template <int G>
-GDEV void fin_put(const Workspace& ws, uint64_t idx, const double* y, const RayConst& rc) {
+GDEV double observer_energy(const DevScene& S, const WorkList& wl, uint64_t idx) {
+  double row, col, p[4];
+  ray_pixel(wl, idx, &row, &col);
+  const DevCamera& cam = S.cam;
+  camera_momentum(cam, row, col, p);
+  return inner<G>(S, cam.pos, cam.sin_theta, cam.cos_theta, cam.vel, p);
+}
+
+// The record of a ray (Workspace::fin, 8 doubles = one 64-B line, written whole by the
+// lane that ends it): what the shade kernel reads of the final state and the ray
+// constants, and the ray's counts.
+//   Schwarzschild, Kerr-Schild, flat charts: y[1..7] (y[0] is not read; Kerr-Schild's
+//   momentum needs none of E, L_z, Q), then the candidate count (low 32 bits), stop
+//   reason and status (bits 32-39, 40-47).  The observer energy is not stored: the shade
+//   kernel recomputes it from the ray's pixel (observer_energy: init_ray's operations on
+//   the same operands, hence the same bits), and the step count goes straight to the
+//   optional per-pixel output (Workspace::steps).
+//   KerrBL: r, theta, phi, v_r, v_theta, observer energy, E, L_z (y[6], y[7] are
+//   identically 0, Q only drives the RHS), and the counts in a 16-B meta record.  The
+//   one-record layout measured C3 +8% (its 3-wave kernel's spills moved into the
+//   accepted-step path: profiles/r04r), so KerrBL keeps this one.
+struct RayMeta {
+  uint32_t nrec, steps;
+  int stop, status;
+};
+template <int G>
+GDEV void fin_put(const Workspace& ws, uint64_t idx, const double* y, const RayConst& rc, uint32_t nrec, int stop,
+                  int status) {
   double v[8];
   if constexpr (G == GRT_GEOM_KERR_BL) {
 #pragma unroll
@@ -1505,36 +1548,15 @@ GDEV void fin_put(const Workspace& ws, uint64_t idx, const double* y, const RayC
   } else {
 #pragma unroll
     for (int k = 0; k < 7; ++k) v[k] = y[1 + k];
-    v[7] = rc.obs;
+    v[7] = __hiloint2double((int)((uint32_t)(stop & 0xff) | ((uint32_t)(status & 0xff) << 8)), (int)nrec);
   }
   double2* d = reinterpret_cast<double2*>(ws.fin + idx * 8);
-#if GRT_FIN_CONST_AT_START
-  if constexpr (G == GRT_GEOM_KERR_BL) {
-    d[0] = make_double2(v[0], v[1]);
-    d[1] = make_double2(v[2], v[3]);
-    ws.fin[idx * 8 + 4] = v[4];
-  } else {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) d[k] = make_double2(v[2 * k], v[2 * k + 1]);
-    ws.fin[idx * 8 + 6] = v[6];
-  }
-#else
 #pragma unroll
   for (int k = 0; k < 4; ++k) d[k] = make_double2(v[2 * k], v[2 * k + 1]);
-#endif
 }
-// The ray constants' part of the record, at the ray's start (GRT_FIN_CONST_AT_START)
+// rc.obs: KerrBL's from the record, else 0 (the caller sets observer_energy)
 template <int G>
-GDEV void fin_put_const(const Workspace& ws, uint64_t idx, const RayConst& rc) {
-  if constexpr (G == GRT_GEOM_KERR_BL) {
-    ws.fin[idx * 8 + 5] = rc.obs;
-    reinterpret_cast<double2*>(ws.fin + idx * 8)[3] = make_double2(rc.e, rc.lz);
-  } else {
-    ws.fin[idx * 8 + 7] = rc.obs;
-  }
-}
-template <int G>
-GDEV void fin_get(const Workspace& ws, uint64_t idx, double* y, RayConst& rc) {
+GDEV RayMeta fin_get(const Workspace& ws, uint64_t idx, double* y, RayConst& rc) {
   const double2* d = reinterpret_cast<const double2*>(ws.fin + idx * 8);
   double v[8];
 #pragma unroll
@@ -1555,31 +1577,31 @@ GDEV void fin_get(const Workspace& ws, uint64_t idx, double* y, RayConst& rc) {
     rc.obs = v[5];
     rc.e = v[6];
     rc.lz = v[7];
+    const uint4 m = reinterpret_cast<const uint4*>(ws.meta)[idx];
+    return RayMeta{m.y, m.x, (int)(m.z & 0xffu), (int)((m.z >> 8) & 0xffu)};
   } else {
 #pragma unroll
     for (int k = 0; k < 7; ++k) y[1 + k] = v[k];
-    rc.obs = v[7];
+    rc.obs = 0.0;
     rc.e = 0.0;
     rc.lz = 0.0;
+    const uint64_t m = (uint64_t)__double_as_longlong(v[7]);
+    return RayMeta{(uint32_t)m, 0u, (int)((m >> 32) & 0xffu), (int)((m >> 40) & 0xffu)};
   }
 }
-struct RayMeta {
-  uint32_t steps, nrec;
-  int stop, status;
-};
-GDEV RayMeta meta_get(const Workspace& ws, uint64_t idx) {
-  const uint4 m = reinterpret_cast<const uint4*>(ws.meta)[idx];
-  return RayMeta{m.x, m.y, (int)(m.z & 0xffu), (int)((m.z >> 8) & 0xffu)};
-}
 
-// End of a ray: its final state and counts go to the workspace for the shade kernel.
+// End of a ray: its record goes to the workspace for the shade kernel.
 template <int G>
 GDEV void store_ray(const Workspace& ws, uint64_t idx, const double* y, const RayConst& rc, int stop, int status,
                     uint32_t nrec, uint32_t steps) {
   RAY_TIME(ws.n, idx, 2, __builtin_amdgcn_s_memrealtime());
-  fin_put<G>(ws, idx, y, rc);
-  reinterpret_cast<uint4*>(ws.meta)[idx] =
-      make_uint4(steps, nrec, (uint32_t)(stop & 0xff) | ((uint32_t)(status & 0xff) << 8), 0u);
+  fin_put<G>(ws, idx, y, rc, nrec, stop, status);
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    reinterpret_cast<uint4*>(ws.meta)[idx] =
+        make_uint4(steps, nrec, (uint32_t)(stop & 0xff) | ((uint32_t)(status & 0xff) << 8), 0u);
+  } else {
+    if (ws.steps) ws.steps[idx] = steps;
+  }
 }
 
 // Candidate nrec >= GRT_WS_SLOTS of ray idx: one record appended to the hit pool and
@@ -1822,11 +1844,8 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
           double row, col;
           bool valid = true;
           if (wl.pixel_index) {  // offset list (get_ray_for_offset, camera.rs:247-254)
-            uint32_t pix = wl.pixel_index[item];
-            double r = (double)(wl.row0 + pix / wl.cols), cc = (double)(wl.col0 + pix % wl.cols);
-            row = r + (wl.dy[item] - 0.5);
-            col = cc + (wl.dx[item] - 0.5);
             idx = item;
+            ray_pixel(wl, idx, &row, &col);
           } else {  // 8x8 pixel tiles, row-major tiles: a wave starts on a compact patch
             uint64_t tile = item >> 6;
             if (wl.tile_order) tile = wl.tile_order[tile];  // longest-predicted tiles first
@@ -1834,15 +1853,13 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
             uint32_t tr = (uint32_t)(tile / wl.tiles_x), tc = (uint32_t)(tile % wl.tiles_x);
             uint32_t r = tr * 8 + (w >> 3), cc = tc * 8 + (w & 7);
             valid = (r < wl.rows) && (cc < wl.cols);
+            // ray_pixel's rectangle / shard case, from (r, cc) directly
             row = (double)(wl.row0 + shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, r));
             col = (double)(wl.col0 + cc);
             idx = (uint64_t)r * wl.cols + cc;
           }
           if (valid) {
             init_ray<G, VOL>(S, row, col, y, rc);
-#if GRT_FIN_CONST_AT_START
-            fin_put_const<G>(ws, idx, rc);
-#endif
             if constexpr (VOL) {  // the raymarch's frequency data (march_kernel)
               ws.rc[0 * n + idx] = rc.obs;
               ws.rc[1 * n + idx] = rc.e;
@@ -2545,8 +2562,8 @@ GDEV int shade_record(const DevScene& S, const RayConst& rc, const DevObject& o,
   return GRT_OK;
 }
 
-GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, int status, int stop,
-                    uint32_t steps, uint32_t hits) {
+// (the step count goes to out.steps from store_ray, KerrBL's from shade_kernel)
+GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, int status, int stop, uint32_t hits) {
   if (out.hits) out.hits[idx] = hits;
   reinterpret_cast<float4*>(out.xyza)[idx] = make_float4((float)c.x, (float)c.y, (float)c.z, (float)c.a);
   out.cls[idx] = (uint8_t)cls;
@@ -2558,7 +2575,6 @@ GDEV void write_out(const Outputs& out, uint64_t idx, const XYZA& c, int cls, in
     d[2] = c.z;
     d[3] = c.a;
   }
-  if (out.steps) out.steps[idx] = steps;
   if (out.stop) out.stop[idx] = (uint8_t)stop;
 }
 
@@ -2613,12 +2629,12 @@ GDEV uint32_t rec_read(const Workspace& ws, const RecRef& r, double* p, double* 
 // error (an error aborts the pixel, scene.rs:146, so its marches would be wasted).
 // Workspace slots come back as a mask; pool records get their jobs appended here.
 template <int G>
-GDEV uint32_t march_slots(const DevScene& S, const Workspace& ws, uint64_t idx) {
-  const RayMeta mt = meta_get(ws, idx);
-  if (mt.status != GRT_OK) return 0u;
+GDEV uint32_t march_slots(const DevScene& S, const WorkList& wl, const Workspace& ws, uint64_t idx) {
   RayConst rc;
   double y[8];
-  fin_get<G>(ws, idx, y, rc);
+  const RayMeta mt = fin_get<G>(ws, idx, y, rc);
+  if (mt.status != GRT_OK) return 0u;
+  if constexpr (G != GRT_GEOM_KERR_BL) rc.obs = observer_energy<G>(S, wl, idx);
   bool lost;
   const uint32_t nr = rec_count(ws, idx, mt.nrec, &lost);
   uint32_t mask = 0u, pool_jobs = 0u, pos = HIT_NIL;
@@ -2654,8 +2670,8 @@ GDEV uint32_t march_slots(const DevScene& S, const Workspace& ws, uint64_t idx) 
 //   MODE 1: volumetric scenes, pass 1 -- append the raymarch jobs (wave-aggregated).
 //   MODE 2: volumetric scenes, pass 3 -- composite with the raymarched colours (ws.vcol).
 template <int G, int MODE>
-__global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__ Sp, Workspace ws, Outputs out,
-                                                    unsigned long long* __restrict__ stats) {
+__global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__ Sp, WorkList wl, Workspace ws,
+                                                    Outputs out, unsigned long long* __restrict__ stats) {
   const DevScene& S = *Sp;
   const uint64_t n = ws.n;
   const uint64_t n_live = ws.n_live ? (uint64_t)min((unsigned long long)n, *ws.n_live) : n;
@@ -2665,7 +2681,7 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
   glibc::tables_to_lds();  // whole block, before the early return
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if constexpr (MODE == 1) {
-    const uint32_t mask = idx < n_live ? march_slots<G>(S, ws, idx) : 0u;
+    const uint32_t mask = idx < n_live ? march_slots<G>(S, wl, ws, idx) : 0u;
     const int lane = threadIdx.x & 63;
     const uint32_t c = __popc(mask);
     uint32_t incl = c;  // inclusive wave prefix sum of the job counts
@@ -2684,18 +2700,20 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(ws.pool->count + 1, *ws.pool->count);
   if (idx >= n_live) return;
-  const RayMeta mt = meta_get(ws, idx);
-  int status = mt.status;
-  const int stop = mt.stop;
-  const uint32_t steps = mt.steps;
-  const XYZA fail{0.0, 0.0, 0.0, 1.0};
-  if (status != GRT_OK) {  // integrate error: reference default pixel (raytracer.rs:204-210)
-    write_out(out, idx, fail, GRT_CLASS_ESCAPED, status, stop, steps, 0u);
-    return;
-  }
   RayConst rc;
   double y[8];
-  fin_get<G>(ws, idx, y, rc);
+  const RayMeta mt = fin_get<G>(ws, idx, y, rc);
+  int status = mt.status;
+  const int stop = mt.stop;
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    if (out.steps) out.steps[idx] = mt.steps;  // the other charts: written by store_ray
+  }
+  const XYZA fail{0.0, 0.0, 0.0, 1.0};
+  if (status != GRT_OK) {  // integrate error: reference default pixel (raytracer.rs:204-210)
+    write_out(out, idx, fail, GRT_CLASS_ESCAPED, status, stop, 0u);
+    return;
+  }
+  if constexpr (G != GRT_GEOM_KERR_BL) rc.obs = observer_energy<G>(S, wl, idx);
   bool lost;
   const uint32_t nr = rec_count(ws, idx, mt.nrec, &lost);
   // window-nearest hits: the first ones in registers, the later ones (pool records of
@@ -2711,8 +2729,7 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     XYZA col{0.0, 0.0, 0.0, 0.0};
     int e = shade_record<G>(S, rc, o, p, pt, &col);
     if (e != GRT_OK) {  // any window error aborts the pixel (scene.rs:146, objects.rs:96-102)
-      write_out(out, idx, fail, GRT_CLASS_ESCAPED, e | (lost ? GRT_FLAG_HIT_OVERFLOW : 0), stop, steps,
-                nh + n_pool_hits);
+      write_out(out, idx, fail, GRT_CLASS_ESCAPED, e | (lost ? GRT_FLAG_HIT_OVERFLOW : 0), stop, nh + n_pool_hits);
       if (lost) atomicAdd(stats + 3, 1ull);
       return;
     }
@@ -2780,7 +2797,7 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
     status |= GRT_FLAG_HIT_OVERFLOW;
     atomicAdd(stats + 3, 1ull);
   }
-  write_out(out, idx, result, cls, status, stop, steps, nh + n_pool_hits);
+  write_out(out, idx, result, cls, status, stop, nh + n_pool_hits);
 }
 
 // ------------------------------------------------------------------ launch -------
@@ -2788,10 +2805,12 @@ __global__ void __launch_bounds__(256) shade_kernel(const DevScene* __restrict__
 // gather raymarch jobs -> march (persistent, lane refill) -> composite; ws.march must be
 // zeroed.  The tail (Kerr-Schild) continues the long rays the integrate kernel handed off.
 template <int G>
-static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws, const Outputs& out,
+static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Workspace& ws_in, const Outputs& out,
                            unsigned long long* d_counter, unsigned long long* d_stats, int blocks, int threads,
                            bool vol, const TailList& tl_in, int tail_blocks, hipStream_t stream) {
-  const unsigned nb = (unsigned)((ws.n + 255) / 256);
+  const unsigned nb = (unsigned)((ws_in.n + 255) / 256);
+  Workspace ws = ws_in;
+  ws.steps = G == GRT_GEOM_KERR_BL ? nullptr : out.steps;  // store_ray writes the per-pixel step counts
   TailList tl = tl_in;
   if (G != GRT_GEOM_KERR || tail_blocks <= 0) tl.cap = 0;
   if (!vol) {
@@ -2806,7 +2825,7 @@ static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Wo
         if ((e = hipGetLastError()) != hipSuccess) return e;
       }
     }
-    hipLaunchKernelGGL((shade_kernel<G, 0>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+    hipLaunchKernelGGL((shade_kernel<G, 0>), dim3(nb), dim3(256), 0, stream, d_scene, wl, ws, out, d_stats);
     return hipGetLastError();
   }
   if (!ws.rec_dir || !ws.vcol || !ws.jobs || !ws.march) return hipErrorInvalidValue;
@@ -2820,11 +2839,11 @@ static hipError_t launch_g(const DevScene* d_scene, const WorkList& wl, const Wo
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
   }
-  hipLaunchKernelGGL((shade_kernel<G, 1>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+  hipLaunchKernelGGL((shade_kernel<G, 1>), dim3(nb), dim3(256), 0, stream, d_scene, wl, ws, out, d_stats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL((march_kernel<G>), dim3(blocks), dim3(256), 0, stream, d_scene, ws);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL((shade_kernel<G, 2>), dim3(nb), dim3(256), 0, stream, d_scene, ws, out, d_stats);
+  hipLaunchKernelGGL((shade_kernel<G, 2>), dim3(nb), dim3(256), 0, stream, d_scene, wl, ws, out, d_stats);
   return hipGetLastError();
 }
 
