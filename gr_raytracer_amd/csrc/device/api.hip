@@ -310,8 +310,12 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     ds.div_share = (std::fpclassify(d.radius) == FP_NORMAL && ex > -500 && ex < 500) ? 1 : 0;
     int ea = 0;
     std::frexp(d.a, &ea);
-    const bool a_ok = d.geometry != GRT_GEOM_KERR_BL || (std::fpclassify(d.a) == FP_NORMAL && ea > -50 && ea < 50);
-    ds.div_fast = (std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -50 && ex < 50 && a_ok) ? 1 : 0;
+    // KerrBL: a normal |a| within 2^+-50; Kerr-Schild (ks_fd_ok): radius and a normal
+    // within 2^+-20, or a == 0
+    const int lim = d.geometry == GRT_GEOM_KERR ? 20 : 50;
+    const bool a_mod = std::fpclassify(d.a) == FP_NORMAL && ea > -lim && ea < lim;
+    const bool a_ok = d.geometry == GRT_GEOM_KERR_BL ? a_mod : (d.geometry != GRT_GEOM_KERR || a_mod || d.a == 0.0);
+    ds.div_fast = (std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -lim && ex < lim && a_ok) ? 1 : 0;
   }
   {  // exact controller shortcuts (geodesic.hip step_control); off unless epsilon is a moderate normal
     int ex = 0;

@@ -75,7 +75,7 @@ struct DevScene {
   // horizon test thresholds, evaluated on the host exactly as the reference does
   double horizon_r;     // Schwarzschild: radius + eps; Kerr/KerrBL: r_plus + eps
   int32_t has_horizon;  // Kerr/KerrBL: |a| <= M
-  int32_t div_fast;     // radius > 0 (and KerrBL's |a|) within 2^+-50: region-B RHS may use div_inrange
+  int32_t div_fast;     // radius > 0 (and a) in range: the range-free divisions may run (api.hip)
   uint64_t max_steps;
   double max_radius_sq, step_size, epsilon;
   double trapped_radius;  // TRAPPED_ORBIT_RADIUS_FACTOR * radius

@@ -52,6 +52,9 @@ namespace grt {
 #ifndef GRT_FAST_DIV
 #define GRT_FAST_DIV 1  // Schwarzschild / KerrBL region-B RHS: divisions without range steps when the operands allow
 #endif
+#ifndef GRT_FAST_DIV_KS
+#define GRT_FAST_DIV_KS 1  // Kerr-Schild RHS: metric quotients without v_div_scale when the state allows
+#endif
 #ifndef GRT_FAST_DIV_BL
 // KerrBL too: C3 is no faster with it (165-172 ms either way), but its 3-wave kernel's
 // spills land elsewhere: 1.71 GB written per frame with it, 20.9 GB without
@@ -177,9 +180,24 @@ GDEV void div2_inrange(double x1, double x2, double y, double* q1, double* q2) {
 // |x| in (2^-300, 2^300), NaN excluded: two compares with the abs modifier
 GDEV bool in_div_range(double x) { return fabs(x) > 0x1p-300 && fabs(x) < 0x1p300; }
 
-// Device check of div_inrange / div2_inrange against the compiler's division: n random
-// pairs (splitmix64) with |x|, |y| in 2^-300 .. 2^300, both signs; counts[0] = pairs
-// whose bits differ.
+// x / y as the compiler's expansion without its two v_div_scale steps but with
+// v_div_fixup: exact (the same instructions on the same values) when y is a normal within
+// 2^+-600 and x is 0 or a normal with |x|, |x / y| within 2^+-600 -- v_div_scale would
+// return its operand unchanged with no flag (so v_div_fmas is a plain fma), and
+// v_div_fixup rewrites the zero-numerator case from the operands alone (a -0 / y chain
+// gives +0; the fixup returns the signed zero).  9 VALU instead of 11.
+GDEV double div_fx(double x, double y) {
+  const double rcp = __builtin_amdgcn_rcp(y);
+  const double fma0 = __builtin_fma(-y, rcp, 1.0);
+  const double fma1 = __builtin_fma(rcp, fma0, rcp);
+  const double fma2 = __builtin_fma(-y, fma1, 1.0);
+  const double fma3 = __builtin_fma(fma1, fma2, fma1);
+  const double m = x * fma3;
+  return __builtin_amdgcn_div_fixup(__builtin_fma(__builtin_fma(-y, m, x), fma3, m), y, x);
+}
+// Device check of div_inrange / div2_inrange / div_fx against the compiler's division: n
+// random pairs (splitmix64) with |x|, |y| in 2^-300 .. 2^300, both signs, and for div_fx
+// also x = +-0; counts[0] = pairs whose bits differ.
 __global__ void div_check_kernel(uint64_t n, uint64_t seed, unsigned long long* counts) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -201,11 +219,24 @@ __global__ void div_check_kernel(uint64_t n, uint64_t seed, unsigned long long* 
   double q1, q2;
   div2_inrange(x, x2, y, &q1, &q2);
   const double q0 = div_inrange(x, y);
+  const double xz = (u >> 61) == 0 ? ((u >> 60) & 1 ? -0.0 : 0.0) : x;  // 1 in 8: a signed zero
+  volatile double vxz = xz;
+  const double ref3 = vxz / vy, q3 = div_fx(xz, y);
   const bool bad = __double_as_longlong(q0) != __double_as_longlong(ref1) ||
                    __double_as_longlong(q1) != __double_as_longlong(ref1) ||
-                   __double_as_longlong(q2) != __double_as_longlong(ref2);
+                   __double_as_longlong(q2) != __double_as_longlong(ref2) ||
+                   __double_as_longlong(q3) != __double_as_longlong(ref3);
   if (bad) atomicAdd(counts, 1ull);
 }
+
+// Kerr-Schild metric quotients: the compiler's division, or div_fx (FD) where the caller
+// has established ks_fd_ok for the state
+template <bool FD>
+GDEV double kdiv(double x, double y) {
+  if constexpr (FD) return div_fx(x, y);
+  else return x / y;
+}
+
 
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
@@ -281,14 +312,15 @@ GDEV double ks_r_sqr(double a, double x, double y, double z) {
   return 0.5 * (rho_sqr - a * a + sqrt((rho_sqr - a * a) * (rho_sqr - a * a) + 4.0 * a * a * z * z));
 }
 // metric(): symmetric by construction; returns the 10 distinct entries in g.
+template <bool FD = false>
 GDEV void ks_metric(double radius, double a, double x, double y, double z, double g[4][4]) {
   double r_sqr = ks_r_sqr(a, x, y, z);
   double r = sqrt(r_sqr);
-  double f = (r * r * r * radius) / (r * r * r * r + a * a * z * z);
+  double f = kdiv<FD>(r * r * r * radius, r * r * r * r + a * a * z * z);
   double k_0 = 1.0;
-  double k_x = (r * x + a * y) / (r_sqr + a * a);
-  double k_y = (r * y - a * x) / (r_sqr + a * a);
-  double k_z = z / r;
+  double k_x = kdiv<FD>(r * x + a * y, r_sqr + a * a);
+  double k_y = kdiv<FD>(r * y - a * x, r_sqr + a * a);
+  double k_z = kdiv<FD>(z, r);
   g[0][0] = k_0 * k_0 * f - 1.0;
   g[0][1] = k_0 * k_x * f;
   g[0][2] = k_0 * k_y * f;
@@ -306,15 +338,16 @@ GDEV void ks_metric(double radius, double a, double x, double y, double z, doubl
   g[3][1] = g[1][3];
   g[3][2] = g[2][3];
 }
+template <bool FD = false>
 GDEV void ks_metric_contra(double radius, double a, double x, double y, double z, double g[4][4]) {
   double r_sqr = ks_r_sqr(a, x, y, z);
   double r = sqrt(r_sqr);
-  double f = (r * r * r * radius) / (r * r * r * r + a * a * z * z);
+  double f = kdiv<FD>(r * r * r * radius, r * r * r * r + a * a * z * z);
   double kc[4];
   kc[0] = -1.0;
-  kc[1] = (r * x + a * y) / (r_sqr + a * a);
-  kc[2] = (r * y - a * x) / (r_sqr + a * a);
-  kc[3] = z / r;
+  kc[1] = kdiv<FD>(r * x + a * y, r_sqr + a * a);
+  kc[2] = kdiv<FD>(r * y - a * x, r_sqr + a * a);
+  kc[3] = kdiv<FD>(z, r);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -347,20 +380,21 @@ GDEV double quad_form(const double* v, const double M[4][4], const double* w) {
 
 // kerr.rs:149-186 + :228-235: returns 0.5 * p^T (G dG_i G) p, which equals
 // -0.5 * p^T d_matrix_contravariant(i) p exactly (negation commutes with rounding).
+template <bool FD = false>
 GDEV double ks_accel(double radius, double a, int index, double x, double y, double z,
                      const double G[4][4], const double* p) {
   double c = index == 1 ? x : (index == 2 ? y : z);
   double h = 1e-10 * fmax(fabs(c), 1.0);
   double dx = index == 1 ? h : 0.0, dy = index == 2 ? h : 0.0, dz = index == 3 ? h : 0.0;
   double mp[4][4], mm[4][4];
-  ks_metric(radius, a, x + dx, y + dy, z + dz, mp);
-  ks_metric(radius, a, x - dx, y - dy, z - dz, mm);
+  ks_metric<FD>(radius, a, x + dx, y + dy, z + dz, mp);
+  ks_metric<FD>(radius, a, x - dx, y - dy, z - dz, mm);
   double two_h = 2.0 * h;
   double D[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) D[i][j] = (mp[i][j] - mm[i][j]) / two_h;
+    for (int j = 0; j < 4; ++j) D[i][j] = kdiv<FD>(mp[i][j] - mm[i][j], two_h);
   double GD[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -451,6 +485,21 @@ GDEV void with_sincos(double theta, bool fast_ok, F&& body, bool div_ok = false)
   double st, ct;
   rsincos(theta, &st, &ct);
   body(st, ct, false, std::false_type{});
+}
+
+// Whether every quotient of rhs<KERR> at state (x, y, z) is in div_fx's range.  With each
+// coordinate 0 or within 2^-100 .. 2^10 and x^2 + y^2 + z^2 - a^2 >= 2^-10 (so r^2 >= 2^-10
+// at the state and >= 2^-11 at the finite-difference points, which move one coordinate by
+// h = 1e-10 max(|c|, 1) <= 2^-23, leaving it 0 or >= 2^-86), and S.div_fast (Kerr-Schild:
+// radius within 2^+-20, a 0 or within 2^+-20): r within 2^-5.5 .. 2^11; f in 2^-97 .. 2^75;
+// the numerators r x + a y, r y - a x are 0 or >= 2^-172 (a nonzero sum of two terms of at
+// least 2^-120 is at least an ulp of the smaller), so k_x, k_y, k_z are 0 or within
+// 2^-212 .. 2^32; metric entries 0 or within 2^-521 .. 2^139 (the diagonal near 1); and
+// (mp - mm) / 2h has a numerator 0 or >= 2^-573 and 2h within 2^-33 .. 2^-22.  Every
+// operand and quotient is 0 or within 2^+-600.
+GDEV bool ks_fd_ok(double a, double x, double y, double z) {
+  auto c_ok = [](double c) { return (c == 0.0) | ((fabs(c) >= 0x1p-100) & (fabs(c) < 0x1p10)); };
+  return c_ok(x) & c_ok(y) & c_ok(z) & (x * x + y * y + z * z - a * a >= 0x1p-10);
 }
 
 // ---- the ODE right-hand sides ----
@@ -567,18 +616,30 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     double radius = S.radius, a = S.a;
     double x = y[1], yy = y[2], z = y[3];
     double p[4] = {y[4], y[5], y[6], y[7]};
-    double Gc[4][4];
-    ks_metric_contra(radius, a, x, yy, z, Gc);
-    double xdot[4];
-    mat_vec(Gc, p, xdot);
-    o[0] = xdot[0];
-    o[1] = xdot[1];
-    o[2] = xdot[2];
-    o[3] = xdot[3];
-    o[4] = 0.0;
-    o[5] = ks_accel(radius, a, 1, x, yy, z, Gc, p);
-    o[6] = ks_accel(radius, a, 2, x, yy, z, Gc, p);
-    o[7] = ks_accel(radius, a, 3, x, yy, z, Gc, p);
+    auto body = [&](auto fd) {
+      constexpr bool FD = decltype(fd)::value;
+      double Gc[4][4];
+      ks_metric_contra<FD>(radius, a, x, yy, z, Gc);
+      double xdot[4];
+      mat_vec(Gc, p, xdot);
+      o[0] = xdot[0];
+      o[1] = xdot[1];
+      o[2] = xdot[2];
+      o[3] = xdot[3];
+      o[4] = 0.0;
+      o[5] = ks_accel<FD>(radius, a, 1, x, yy, z, Gc, p);
+      o[6] = ks_accel<FD>(radius, a, 2, x, yy, z, Gc, p);
+      o[7] = ks_accel<FD>(radius, a, 3, x, yy, z, Gc, p);
+    };
+#if GRT_FAST_DIV_KS
+    // The metric quotients without v_div_scale (div_fx) when every lane's state passes
+    // ks_fd_ok (wave-uniform, like the region-B forms above)
+    if (S.div_fast && __ballot(!ks_fd_ok(a, x, yy, z)) == 0) {
+      body(std::true_type{});
+      return;
+    }
+#endif
+    body(std::false_type{});
   } else {  // Euclidean, euclidean.rs:47-53
     o[0] = y[4];
     o[1] = y[5];

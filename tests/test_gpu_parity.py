@@ -372,9 +372,11 @@ def test_row_shards_reassemble_the_frame(grt, gpu, n_shards, band_rows):
 
 
 def test_division_in_range(grt):
-    """The speculative attempt's divisions (geodesic.hip div_inrange / div2_inrange: the
-    compiler's f64 division expansion without its range steps) return the compiler's
-    division bits on 16M random operand pairs with |x|, |y| in 2^-300 .. 2^300."""
+    """The range-free divisions (geodesic.hip div_inrange / div2_inrange: the compiler's
+    f64 division expansion without its range steps, used by the region-B RHS; div_fx:
+    without v_div_scale but with v_div_fixup, used by the Kerr-Schild RHS) return the
+    compiler's division bits on 2 x 16M random operand pairs with |x|, |y| in
+    2^-300 .. 2^300 (div_fx also with signed-zero numerators)."""
     import ctypes as C
 
     lib = grt.lib()
