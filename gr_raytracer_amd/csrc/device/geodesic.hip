@@ -55,6 +55,9 @@ namespace grt {
 #ifndef GRT_FAST_DIV_KS
 #define GRT_FAST_DIV_KS 1  // Kerr-Schild RHS: metric quotients without v_div_scale when the state allows
 #endif
+#ifndef GRT_FAST_SQRT_KS
+#define GRT_FAST_SQRT_KS 1  // and its square roots without the range steps (sqrt_fx)
+#endif
 #ifndef GRT_FAST_DIV_BL
 // KerrBL too: C3 is no faster with it (165-172 ms either way), but its 3-wave kernel's
 // spills land elsewhere: 1.71 GB written per frame with it, 20.9 GB without
@@ -195,7 +198,37 @@ GDEV double div_fx(double x, double y) {
   const double m = x * fma3;
   return __builtin_amdgcn_div_fixup(__builtin_fma(__builtin_fma(-y, m, x), fma3, m), y, x);
 }
-// Device check of div_inrange / div2_inrange / div_fx against the compiler's division: n
+
+// Kerr-Schild metric quotients: the compiler's division, or div_fx (FD) where the caller
+// has established ks_fd_ok for the state
+template <bool FD>
+GDEV double kdiv(double x, double y) {
+  if constexpr (FD) return div_fx(x, y);
+  else return x / y;
+}
+// sqrt(x) as the compiler's f64 expansion for gfx950 without its range steps: for a
+// normal x >= 2^-767 the input scaling (ldexp by 0), the output rescaling and the
+// zero / infinity select are identities, leaving v_rsq_f64 and the Newton steps on the
+// same values, hence sqrt's bits (device check: test_division_in_range).  10 VALU
+// instead of 17.
+GDEV double sqrt_fx(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+template <bool FD>
+GDEV double ksqrt(double x) {
+  if constexpr (FD && GRT_FAST_SQRT_KS) return sqrt_fx(x);
+  else return sqrt(x);
+}
+
+// Device check of div_inrange / div2_inrange / div_fx / sqrt_fx against the compiler's division and sqrt: n
 // random pairs (splitmix64) with |x|, |y| in 2^-300 .. 2^300, both signs, and for div_fx
 // also x = +-0; counts[0] = pairs whose bits differ.
 __global__ void div_check_kernel(uint64_t n, uint64_t seed, unsigned long long* counts) {
@@ -222,19 +255,16 @@ __global__ void div_check_kernel(uint64_t n, uint64_t seed, unsigned long long* 
   const double xz = (u >> 61) == 0 ? ((u >> 60) & 1 ? -0.0 : 0.0) : x;  // 1 in 8: a signed zero
   volatile double vxz = xz;
   const double ref3 = vxz / vy, q3 = div_fx(xz, y);
+  const double sx = fabs(x) * 0x1p-300;  // sqrt_fx: 2^-600 .. 2^0 as well as 2^-300 .. 2^300
+  volatile double vsx = sx, vax = fabs(x);
+  const double ref4 = sqrt(vsx), ref5 = sqrt(vax);
   const bool bad = __double_as_longlong(q0) != __double_as_longlong(ref1) ||
                    __double_as_longlong(q1) != __double_as_longlong(ref1) ||
                    __double_as_longlong(q2) != __double_as_longlong(ref2) ||
-                   __double_as_longlong(q3) != __double_as_longlong(ref3);
+                   __double_as_longlong(q3) != __double_as_longlong(ref3) ||
+                   __double_as_longlong(sqrt_fx(sx)) != __double_as_longlong(ref4) ||
+                   __double_as_longlong(sqrt_fx(fabs(x))) != __double_as_longlong(ref5);
   if (bad) atomicAdd(counts, 1ull);
-}
-
-// Kerr-Schild metric quotients: the compiler's division, or div_fx (FD) where the caller
-// has established ks_fd_ok for the state
-template <bool FD>
-GDEV double kdiv(double x, double y) {
-  if constexpr (FD) return div_fx(x, y);
-  else return x / y;
 }
 
 
@@ -307,15 +337,16 @@ struct RayConst {
 
 // =========================================================== geometry kernels ======
 // ---- Kerr-Schild helpers (kerr.rs:31-110) ----
+template <bool FD = false>
 GDEV double ks_r_sqr(double a, double x, double y, double z) {
   double rho_sqr = x * x + y * y + z * z;
-  return 0.5 * (rho_sqr - a * a + sqrt((rho_sqr - a * a) * (rho_sqr - a * a) + 4.0 * a * a * z * z));
+  return 0.5 * (rho_sqr - a * a + ksqrt<FD>((rho_sqr - a * a) * (rho_sqr - a * a) + 4.0 * a * a * z * z));
 }
 // metric(): symmetric by construction; returns the 10 distinct entries in g.
 template <bool FD = false>
 GDEV void ks_metric(double radius, double a, double x, double y, double z, double g[4][4]) {
-  double r_sqr = ks_r_sqr(a, x, y, z);
-  double r = sqrt(r_sqr);
+  double r_sqr = ks_r_sqr<FD>(a, x, y, z);
+  double r = ksqrt<FD>(r_sqr);
   double f = kdiv<FD>(r * r * r * radius, r * r * r * r + a * a * z * z);
   double k_0 = 1.0;
   double k_x = kdiv<FD>(r * x + a * y, r_sqr + a * a);
@@ -340,8 +371,8 @@ GDEV void ks_metric(double radius, double a, double x, double y, double z, doubl
 }
 template <bool FD = false>
 GDEV void ks_metric_contra(double radius, double a, double x, double y, double z, double g[4][4]) {
-  double r_sqr = ks_r_sqr(a, x, y, z);
-  double r = sqrt(r_sqr);
+  double r_sqr = ks_r_sqr<FD>(a, x, y, z);
+  double r = ksqrt<FD>(r_sqr);
   double f = kdiv<FD>(r * r * r * radius, r * r * r * r + a * a * z * z);
   double kc[4];
   kc[0] = -1.0;
@@ -496,7 +527,8 @@ GDEV void with_sincos(double theta, bool fast_ok, F&& body, bool div_ok = false)
 // least 2^-120 is at least an ulp of the smaller), so k_x, k_y, k_z are 0 or within
 // 2^-212 .. 2^32; metric entries 0 or within 2^-521 .. 2^139 (the diagonal near 1); and
 // (mp - mm) / 2h has a numerator 0 or >= 2^-573 and 2h within 2^-33 .. 2^-22.  Every
-// operand and quotient is 0 or within 2^+-600.
+// operand and quotient is 0 or within 2^+-600.  The square roots (sqrt_fx) take
+// (rho^2 - a^2)^2 + 4 a^2 z^2 >= 2^-22 and r^2 >= 2^-11, both below 2^46.
 GDEV bool ks_fd_ok(double a, double x, double y, double z) {
   auto c_ok = [](double c) { return (c == 0.0) | ((fabs(c) >= 0x1p-100) & (fabs(c) < 0x1p10)); };
   return c_ok(x) & c_ok(y) & c_ok(z) & (x * x + y * y + z * z - a * a >= 0x1p-10);
