@@ -482,6 +482,7 @@ def main() -> None:
         L.check(L.lib().grt_set_launch_config(args.blocks_per_cu, 256), "grt_set_launch_config")
     line = (run_c4 if args.workload == "c4" else run_c2)(args, rank, world, local_rank, dev)
     if line is not None:
+        line["source_hash"] = L.source_stamp()  # the sources libgrt.so was built from (checked on load)
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -157,6 +157,7 @@ def lib() -> C.CDLL:
     sigs = {
         "grt_last_error": (C.c_char_p, []),
         "grt_device_count": (C.c_int, []),
+        "grt_source_hash": (C.c_char_p, []),
         "grt_default_global_opts": (None, [C.POINTER(GlobalOpts)]),
         "grt_default_adaptive_config": (None, [C.POINTER(AdaptiveConfig)]),
         "grt_host_scene_load": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(GlobalOpts), C.POINTER(vp)]),
@@ -235,6 +236,7 @@ def lib() -> C.CDLL:
     }
     # GRT_LIB_ALLOW_MISSING=1 (tools/time_variants.py only) binds an older experimental
     # build that lacks newer entry points; by default a missing symbol is an error.
+    # It also skips the source stamp check below (such a build is not the checkout's).
     allow_missing = os.environ.get("GRT_LIB_ALLOW_MISSING") == "1"
     for name, (res, args) in sigs.items():
         if allow_missing and not hasattr(L, name):
@@ -242,12 +244,32 @@ def lib() -> C.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if not allow_missing:
+        check_source_stamp(L)
     _lib = L
     return L
 
 
+def check_source_stamp(L) -> str:
+    """The library's grt_source_hash() must equal the checkout's source hash
+    (source_hash.py): a prebuilt libgrt.so from other sources is refused."""
+    from .source_hash import source_hash
+
+    stamp = L.grt_source_hash().decode()
+    want = source_hash()
+    if stamp != want:
+        raise GrtError(f"{LIB_PATH} was built from other sources (stamp {stamp[:16]}, checkout {want[:16]}): "
+                       "rebuild it (make -C gr_raytracer_amd/csrc)")
+    return stamp
+
+
+def source_stamp() -> str:
+    """The loaded library's source hash (bench.py and smoke() print it)."""
+    return lib().grt_source_hash().decode()
+
+
 EXPORTED_SYMBOLS = [
-    "grt_last_error", "grt_device_count", "grt_default_global_opts", "grt_default_adaptive_config",
+    "grt_last_error", "grt_device_count", "grt_source_hash", "grt_default_global_opts", "grt_default_adaptive_config",
     "grt_host_scene_load", "grt_host_geometry_load", "grt_host_scene_desc", "grt_host_scene_log", "grt_host_scene_adaptive", "grt_host_scene_destroy",
     "grt_camera_build", "grt_stationary_velocity", "grt_zamo_velocity", "grt_cartesian_to_spherical",
     "grt_cartesian_to_boyer_lindquist", "grt_kerr_temperature_lut", "grt_r_isco", "grt_blackbody_lut",

@@ -316,6 +316,13 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     const bool a_mod = std::fpclassify(d.a) == FP_NORMAL && ea > -lim && ea < lim;
     const bool a_ok = d.geometry == GRT_GEOM_KERR_BL ? a_mod : (d.geometry != GRT_GEOM_KERR || a_mod || d.a == 0.0);
     ds.div_fast = (std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -lim && ex < lim && a_ok) ? 1 : 0;
+    // ks_fd_ok's coordinate bound: 2^ceil(log2(2 max_radius)) covers every state of a ray
+    // (it stops one step beyond max_radius), within the proven 2^10 .. 2^32
+    int em = 0;
+    const double mr2 = 2.0 * d.max_radius;
+    const double m = std::isfinite(mr2) && mr2 > 0.0 ? std::frexp(mr2, &em) : 0.0;
+    if (m == 0.5) em -= 1;  // an exact power of two is its own bound
+    ds.ks_cap = std::ldexp(1.0, !std::isfinite(mr2) ? 32 : std::min(32, std::max(10, em)));
   }
   {  // exact controller shortcuts (geodesic.hip step_control); off unless epsilon is a moderate normal
     int ex = 0;
@@ -551,7 +558,7 @@ int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList*
       dc.tail_mem = nullptr;
     }
     dc.tail_cap = 0;
-    HIP_TRY(hipMalloc(&dc.tail_mem, cap * 17 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dc.tail_mem, cap * 16 * sizeof(unsigned long long)));
     dc.tail_cap = cap;
   }
   tl->ctl = dc.d_tail_ctl;
@@ -766,6 +773,8 @@ int grt_debug_probe_order(grt_scene* s, int device, const grt_row_shard* sh, uin
 int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n, uint64_t* t0) {
   if (!scene || !out || !t0) return fail(-EINVAL, "null argument");
   if (n != g_rt_n || !g_rt) return fail(-EINVAL, "ray count differs from the last trace");
+  if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
+    return fail(-EINVAL, "no trace on this device");
   DeviceCopy& dc = *scene->devices[device];
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipDeviceSynchronize());
@@ -775,23 +784,63 @@ int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n,
 }
 #endif
 
-// Test hook (not in grt_api.h): the range-checked division of the speculative attempt
-// (geodesic.hip div_inrange) against the compiler's f64 division on n random operand
-// pairs; *mismatches = pairs whose bits differ (0 expected).
-int grt_debug_div_check(int device, uint64_t n, uint64_t seed, uint64_t* mismatches) {
-  if (!mismatches || n == 0 || n > (1ull << 32)) return fail(-EINVAL, "div check: 1 <= n <= 2^32");
+// Test hook (not in grt_api.h): the range-free divisions and square root (geodesic.hip
+// div_inrange, div2_inrange, div_fx, sqrt_fx) against the compiler's over the exponent
+// plane (arith_map_kernel): map[2047 * 2047], zmap[2047], smap[2047] flag bytes.
+int grt_debug_arith_map(int device, uint32_t samples, uint64_t seed, uint8_t* map, uint8_t* zmap, uint8_t* smap) {
+  if (!map || !zmap || !smap || samples == 0 || samples > 4096) return fail(-EINVAL, "arith map: 1 <= samples <= 4096");
   HIP_TRY(hipSetDevice(device));
-  unsigned long long* d = nullptr;
-  HIP_TRY(hipMalloc(&d, 8));
-  hipError_t e = hipMemset(d, 0, 8);
-  if (e == hipSuccess) e = grt::launch_div_check(n, seed, d, nullptr);
-  unsigned long long h = 0;
-  if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
-  HIP_TRY(e);
-  *mismatches = h;
+  const size_t nm = 2047u * 2047u;
+  DevBuf b;
+  int rc = b.alloc(nm + 2 * 2047);
+  if (rc) return rc;
+  uint8_t* d = (uint8_t*)b.p;
+  HIP_TRY(hipMemset(d, 0, nm + 2 * 2047));
+  HIP_TRY(grt::launch_arith_map(samples, seed, d, d + nm, d + nm + 2047, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(map, d, nm, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(zmap, d + nm, 2047, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(smap, d + nm + 2047, 2047, hipMemcpyDeviceToHost));
   return 0;
 }
+
+// Test hook (not in grt_api.h): the scene's RHS in its range-free and IEEE forms on n
+// host states (8 doubles each; KerrBL: e, l_z, q per state in consts), out[16 n], pred[n]
+// (rhs_check_kernel).
+int grt_debug_rhs_check(grt_scene* s, int device, uint64_t n, const double* states, const double* consts,
+                        double* out, uint8_t* pred) {
+  if (!s || !states || !out || !pred || n == 0 || n > (1ull << 26)) return fail(-EINVAL, "rhs check: 1 <= n <= 2^26");
+  const int g = s->desc.geometry;
+  if (g != GRT_GEOM_SCHWARZSCHILD && g != GRT_GEOM_KERR && g != GRT_GEOM_KERR_BL)
+    return fail(-EINVAL, "rhs check: Schwarzschild, Kerr-Schild or KerrBL");
+  if (g == GRT_GEOM_KERR_BL && !consts) return fail(-EINVAL, "rhs check: KerrBL needs e, l_z, q per state");
+  DeviceCopy* dc;
+  int rc = ensure_device(s, device, &dc);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  DevBuf b_st, b_c, b_out, b_pred;
+  if ((rc = b_st.alloc(n * 64)) || (rc = b_c.alloc(n * 24)) || (rc = b_out.alloc(n * 128)) || (rc = b_pred.alloc(n)))
+    return rc;
+  HIP_TRY(hipMemcpy(b_st.p, states, n * 64, hipMemcpyHostToDevice));
+  if (consts) HIP_TRY(hipMemcpy(b_c.p, consts, n * 24, hipMemcpyHostToDevice));
+  HIP_TRY(grt::launch_rhs_check(g, dc->d_scene, (const double*)b_st.p, (const double*)b_c.p, n, (double*)b_out.p,
+                                (uint8_t*)b_pred.p, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, b_out.p, n * 128, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(pred, b_pred.p, n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+#if GRT_KS_PATH_COUNT
+// Diagnostic builds only (not in grt_api.h): rhs<KERR> evaluations by form since the last
+// reset: [0] wave-level range-free, [1] wave-level IEEE, [2] / [3] the same in lanes.
+int grt_debug_ks_path(uint64_t* out, int reset) {
+  if (!out) return fail(-EINVAL, "null argument");
+  HIP_TRY(grt::ks_path_read((unsigned long long*)out, reset != 0));
+  return 0;
+}
+#endif
 
 int grt_set_two_ended(int on) {
   if (on != 0 && on != 1) return fail(-EINVAL, "two-ended queue: 0 or 1");

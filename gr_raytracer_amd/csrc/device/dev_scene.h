@@ -76,6 +76,7 @@ struct DevScene {
   double horizon_r;     // Schwarzschild: radius + eps; Kerr/KerrBL: r_plus + eps
   int32_t has_horizon;  // Kerr/KerrBL: |a| <= M
   int32_t div_fast;     // radius > 0 (and a) in range: the range-free divisions may run (api.hip)
+  double ks_cap;        // Kerr-Schild: coordinate bound of ks_fd_ok, a power of two in 2^10 .. 2^32 (api.hip)
   uint64_t max_steps;
   double max_radius_sq, step_size, epsilon;
   double trapped_radius;  // TRAPPED_ORBIT_RADIUS_FACTOR * radius
@@ -239,8 +240,10 @@ struct TailList {
   unsigned long long* ctl;  // 16 words
   uint64_t cap;             // entries of st (0: hand-off disabled)
   uint64_t threshold;       // hand off once the queue is drained and live <= threshold
-  // [17][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,
-  // nrec | retries << 32 | c_valid << 48, observer energy
+  // [16][cap] 64-bit words per entry: y[0..7], c[0..2], h, h_cur, i, output slot,
+  // nrec | retries << 32 | c_valid << 48 (no ray constant: only Kerr-Schild hands off,
+  // and its RHS, momentum and records read none; the shade kernel recomputes the
+  // observer energy from the pixel)
   unsigned long long* st;
 };
 

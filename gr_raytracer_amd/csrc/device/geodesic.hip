@@ -157,8 +157,11 @@ GDEV void div2_same_den(double x1, double x2, double y, double* q1, double* q2) 
 // < 768, neither 1 / y nor x / y is denormal, exp(x) > 53), so v_div_fmas is a plain
 // fma, and v_div_fixup, which only rewrites NaN / infinity / zero / overflow / underflow
 // cases, passes the quotient through.
-// The same instructions on the same values, hence x / y's bits (checked on the device
-// against the compiler's division, tests/test_gpu_parity.py::test_division_in_range).
+// The same instructions on the same values, hence x / y's bits.  Measured over the whole
+// exponent plane, the exact region is larger (E: |y| normal below 2^1022, x of exponent
+// >= -969, gap -1021 .. 1022; the gap >= 768 scaling is an identity there too), and the
+// first failures are one exponent outside it (tests/test_gpu_arith.py
+// ::test_range_free_arithmetic_map, profiles/r05a/arith_map.json).
 // 8 VALU instead of 11; div2_inrange shares 1 / y: 11 instead of 16.
 GDEV double div_inrange(double x, double y) {
   const double rcp = __builtin_amdgcn_rcp(y);
@@ -209,8 +212,8 @@ GDEV double kdiv(double x, double y) {
 // sqrt(x) as the compiler's f64 expansion for gfx950 without its range steps: for a
 // normal x >= 2^-767 the input scaling (ldexp by 0), the output rescaling and the
 // zero / infinity select are identities, leaving v_rsq_f64 and the Newton steps on the
-// same values, hence sqrt's bits (device check: test_division_in_range).  10 VALU
-// instead of 17.
+// same values, hence sqrt's bits (device check: tests/test_gpu_arith.py: exact for every
+// x >= 2^-969, the first failure at 2^-971).  10 VALU instead of 17.
 GDEV double sqrt_fx(double x) {
   const double r = __builtin_amdgcn_rsq(x);
   double g = x * r, h = r * 0.5;
@@ -228,45 +231,60 @@ GDEV double ksqrt(double x) {
   else return sqrt(x);
 }
 
-// Device check of div_inrange / div2_inrange / div_fx / sqrt_fx against the compiler's division and sqrt: n
-// random pairs (splitmix64) with |x|, |y| in 2^-300 .. 2^300, both signs, and for div_fx
-// also x = +-0; counts[0] = pairs whose bits differ.
-__global__ void div_check_kernel(uint64_t n, uint64_t seed, unsigned long long* counts) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// Device check of div_inrange / div2_inrange / div_fx / sqrt_fx against the compiler's
+// division and sqrt over the whole exponent plane (tests/test_gpu_parity.py
+// ::test_range_free_arithmetic_map): thread (ex, ey), ex, ey biased exponents 0 .. 2046
+// (0: subnormals), runs `samples` operand pairs x = +-m_x 2^(ex-1023), y = +-m_y 2^(ey-1023)
+// -- the first four with extreme mantissas (0 / all ones), the rest splitmix64-random, and
+// a second numerator x2 of the same exponent for div2_inrange -- and sets in map[ex][ey]:
+//   1 div_inrange(x, y) != x / y      2 div2_inrange(x, x2, y) != (x / y, x2 / y)
+//   4 div_fx(x, y) != x / y
+// Threads with ex == 0 also set zmap[ey] |= 8 when div_fx(+-0, y) != +-0 / y, and threads
+// with ey == 0 set smap[ex] |= 16 when sqrt_fx(x) != sqrt(x) for positive x of exponent ex.
+__global__ void arith_map_kernel(uint32_t samples, uint64_t seed, uint8_t* map, uint8_t* zmap, uint8_t* smap) {
+  const uint32_t cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell >= 2047u * 2047u) return;
+  const uint32_t ex = cell / 2047u, ey = cell % 2047u;
   auto mix = [](uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
   };
-  const uint64_t u = mix(seed ^ (i * 2 + 1)), v = mix(seed ^ (i * 2 + 2));
-  // exponents: a quarter of the pairs near 1 (the common case), the rest spread
-  const int ex = (u & 3) ? (int)((u >> 52) % 601) - 300 : (int)((u >> 52) % 9) - 4;
-  const int ey = (v & 3) ? (int)((v >> 52) % 601) - 300 : (int)((v >> 52) % 9) - 4;
-  double x = __longlong_as_double((long long)((u & 0x800fffffffffffffull) | ((uint64_t)(1023 + ex) << 52)));
-  double y = __longlong_as_double((long long)((v & 0x800fffffffffffffull) | ((uint64_t)(1023 + ey) << 52)));
-  const double x2 = 2.0 * x;
-  volatile double vx = x, vy = y, vx2 = x2;  // keep the reference divisions as divisions
-  const double ref1 = vx / vy, ref2 = vx2 / vy;
-  double q1, q2;
-  div2_inrange(x, x2, y, &q1, &q2);
-  const double q0 = div_inrange(x, y);
-  const double xz = (u >> 61) == 0 ? ((u >> 60) & 1 ? -0.0 : 0.0) : x;  // 1 in 8: a signed zero
-  volatile double vxz = xz;
-  const double ref3 = vxz / vy, q3 = div_fx(xz, y);
-  const double sx = fabs(x) * 0x1p-300;  // sqrt_fx: 2^-600 .. 2^0 as well as 2^-300 .. 2^300
-  volatile double vsx = sx, vax = fabs(x);
-  const double ref4 = sqrt(vsx), ref5 = sqrt(vax);
-  const bool bad = __double_as_longlong(q0) != __double_as_longlong(ref1) ||
-                   __double_as_longlong(q1) != __double_as_longlong(ref1) ||
-                   __double_as_longlong(q2) != __double_as_longlong(ref2) ||
-                   __double_as_longlong(q3) != __double_as_longlong(ref3) ||
-                   __double_as_longlong(sqrt_fx(sx)) != __double_as_longlong(ref4) ||
-                   __double_as_longlong(sqrt_fx(fabs(x))) != __double_as_longlong(ref5);
-  if (bad) atomicAdd(counts, 1ull);
+  constexpr uint64_t MANT = 0x000fffffffffffffull;
+  auto bits = [](double v) { return (uint64_t)__double_as_longlong(v); };
+  auto make = [](uint64_t sign, uint64_t e, uint64_t m) {
+    return __longlong_as_double((long long)((sign << 63) | (e << 52) | m));
+  };
+  uint32_t flags = 0, zflags = 0, sflags = 0;
+  for (uint32_t k = 0; k < samples; ++k) {
+    const uint64_t u = mix(seed ^ ((uint64_t)cell * 64 + 3 * k + 1)), v = mix(seed ^ ((uint64_t)cell * 64 + 3 * k + 2)),
+                   w = mix(seed ^ ((uint64_t)cell * 64 + 3 * k + 3));
+    const uint64_t mx = k < 4 ? ((k & 1) ? MANT : 0) : (u & MANT);
+    const uint64_t my = k < 4 ? ((k & 2) ? MANT : 0) : (v & MANT);
+    const double x = make(u >> 63, ex, mx), y = make(v >> 63, ey, my), x2 = make(w >> 63, ex, w & MANT);
+    volatile double vx = x, vy = y, vx2 = x2;  // keep the reference divisions as divisions
+    const double ref1 = vx / vy, ref2 = vx2 / vy;
+    double q1, q2;
+    div2_inrange(x, x2, y, &q1, &q2);
+    if (bits(div_inrange(x, y)) != bits(ref1)) flags |= 1u;
+    if (bits(q1) != bits(ref1) || bits(q2) != bits(ref2)) flags |= 2u;
+    if (bits(div_fx(x, y)) != bits(ref1)) flags |= 4u;
+    if (ex == 0) {
+      const double z0 = (u >> 62) & 1 ? -0.0 : 0.0;
+      volatile double vz = z0;
+      if (bits(div_fx(z0, y)) != bits(vz / vy)) zflags |= 8u;
+    }
+    if (ey == 0) {
+      const double sx = fabs(x);
+      volatile double vsx = sx;
+      if (bits(sqrt_fx(sx)) != bits(sqrt(vsx))) sflags |= 16u;
+    }
+  }
+  map[cell] = (uint8_t)flags;
+  if (ex == 0) zmap[ey] = (uint8_t)zflags;
+  if (ey == 0) smap[ex] = (uint8_t)sflags;
 }
-
 
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
@@ -518,24 +536,63 @@ GDEV void with_sincos(double theta, bool fast_ok, F&& body, bool div_ok = false)
   body(st, ct, false, std::false_type{});
 }
 
-// Whether every quotient of rhs<KERR> at state (x, y, z) is in div_fx's range.  With each
-// coordinate 0 or within 2^-100 .. 2^10 and x^2 + y^2 + z^2 - a^2 >= 2^-10 (so r^2 >= 2^-10
-// at the state and >= 2^-11 at the finite-difference points, which move one coordinate by
-// h = 1e-10 max(|c|, 1) <= 2^-23, leaving it 0 or >= 2^-86), and S.div_fast (Kerr-Schild:
-// radius within 2^+-20, a 0 or within 2^+-20): r within 2^-5.5 .. 2^11; f in 2^-97 .. 2^75;
-// the numerators r x + a y, r y - a x are 0 or >= 2^-172 (a nonzero sum of two terms of at
-// least 2^-120 is at least an ulp of the smaller), so k_x, k_y, k_z are 0 or within
-// 2^-212 .. 2^32; metric entries 0 or within 2^-521 .. 2^139 (the diagonal near 1); and
-// (mp - mm) / 2h has a numerator 0 or >= 2^-573 and 2h within 2^-33 .. 2^-22.  Every
-// operand and quotient is 0 or within 2^+-600.  The square roots (sqrt_fx) take
-// (rho^2 - a^2)^2 + 4 a^2 z^2 >= 2^-22 and r^2 >= 2^-11, both below 2^46.
-GDEV bool ks_fd_ok(double a, double x, double y, double z) {
-  auto c_ok = [](double c) { return (c == 0.0) | ((fabs(c) >= 0x1p-100) & (fabs(c) < 0x1p10)); };
-  return c_ok(x) & c_ok(y) & c_ok(z) & (x * x + y * y + z * z - a * a >= 0x1p-10);
+// Whether every quotient and square root of rhs<KERR> at state (x, y, z) is in the exact
+// region of div_fx / sqrt_fx.  That region (measured over the whole exponent plane,
+// tests/test_gpu_arith.py::test_range_free_arithmetic_map) is E: y normal with
+// |y| < 2^1022, x = 0 or of exponent >= -969, exponent gap within -1021 .. 1022; sqrt_fx:
+// x >= 2^-969.  Bound chain, with cap = S.ks_cap <= 2^32 (host: 2^ceil(log2(2 max_radius)),
+// within 2^10 .. 2^32) and S.div_fast (radius within 2^+-20, a = 0 or within 2^+-20):
+//  * the state: each coordinate 0 or 2^-100 <= |c| < cap; D = rho^2 - a^2 >= 2^-10 + 2^-31 rho^2.
+//  * the finite-difference points of ks_accel move one coordinate by h = 1e-10 max(|c|, 1):
+//    it stays 0 / >= 2^-86 / +-1e-10 and <= 2^32, and rho^2 moves by < 2^-32 (rho^2 + 1), so
+//    D >= 2^-11 and rho^2 < 2^66 at every point the metric is evaluated.
+//  * sqrt_fx arguments: D^2 + 4 a^2 z^2 in 2^-22 .. 2^133; r^2 = (D + sqrt(..)) / 2 in
+//    2^-11 .. 2^66 (r^2 <= rho^2), so r in 2^-5.5 .. 2^33.
+//  * f = r^3 radius / (r^4 + a^2 z^2): numerator 2^-36.5 .. 2^119, denominator 2^-22 .. 2^133.
+//  * k_x, k_y: numerator r x + a y is 0, or a nonzero sum of terms >= 2^-120 (>= 2^-172, a
+//    multiple of the smaller term's ulp), <= 2^66; denominator r^2 + a^2 in 2^-11 .. 2^67.
+//    k_z = z / r: numerator 0 or >= 2^-100, denominator 2^-5.5 .. 2^33.  So every k is 0 or
+//    within 2^-239 .. 2^76, f within 2^-170 .. 2^15, metric entries 0 or within 2^-648 .. 2^168.
+//  * D_ij = (mp - mm) / 2h: numerator 0 or >= an ulp of the smaller entry (>= 2^-700), <= 2^169;
+//    2h = 2e-10 max(|c|, 1) within 2^-33 .. 2^0.
+// Every numerator is 0 or of exponent -700 .. 169, every denominator of exponent -33 .. 133:
+// inside E, with the box |x|, |y|, |x / y| <= 2^+-600 of the earlier argument to spare.  The
+// device check of the whole RHS against its IEEE form on states at these edges, cap 2^15 and
+// 2^32: tests/test_gpu_arith.py::test_rhs_kerr_schild_fast_form_matches_ieee.
+GDEV bool ks_fd_ok(double a, double x, double y, double z, double cap) {
+  auto c_ok = [cap](double c) { return (c == 0.0) | ((fabs(c) >= 0x1p-100) & (fabs(c) < cap)); };
+  const double rho2 = x * x + y * y + z * z;
+  return c_ok(x) & c_ok(y) & c_ok(z) & (rho2 - a * a >= 0x1p-10 + 0x1p-31 * rho2);
+}
+// Region-B division predicates of the Schwarzschild and KerrBL RHS (see there)
+GDEV bool schw_div_ok(const DevScene& S, double r) {
+  return S.div_fast && (fabs(r) > 0x1p-100) & (fabs(r) < 0x1p100) & (fabs(r - S.radius) > S.radius * 0x1p-40);
+}
+GDEV bool bl_div_ok(const DevScene& S, double r, double del, double l_z) {
+  return S.div_fast && (fabs(r) < 0x1p100) & in_div_range(del) & (fabs(l_z) > 0x1p-200) & (fabs(l_z) < 0x1p100);
 }
 
+#ifndef GRT_KS_PATH_COUNT
+#define GRT_KS_PATH_COUNT 0  // diagnostic builds only: count rhs<KERR> evaluations per form
+#endif
+#if GRT_KS_PATH_COUNT
+// [0] wave-level fast-form evaluations, [1] IEEE-form, [2] / [3] the same in lanes
+__shared__ unsigned long long ks_path_lds[4];
+__device__ unsigned long long g_ks_path[4];
+GDEV void ks_path_count(int k) {
+  const uint64_t m = __ballot(1);  // the lanes evaluating this RHS together
+  if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) {
+    atomicAdd(&ks_path_lds[k], 1ull);
+    atomicAdd(&ks_path_lds[k + 2], (unsigned long long)__popcll(m));
+  }
+}
+#endif
+
 // ---- the ODE right-hand sides ----
-template <int G>
+// MODE 0: the render's RHS.  MODE 1 / 2 (rhs_check_kernel only): region-B sincos (or no
+// sincos: Kerr-Schild), then the range-free (1) or the IEEE (2) form of the body, whatever
+// the predicates say -- the check compares the two where the predicate holds.
+template <int G, int MODE = 0>
 GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o) {
   if constexpr (G == GRT_GEOM_SCHWARZSCHILD) {  // schwarzschild.rs:54-80
     double radius = S.radius;
@@ -586,10 +643,18 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     // Divisions without range steps (div_inrange) in region B: there sin theta >= 0.75 and
     // 2^-55 < |cos theta| < 0.66, and with S.div_fast (0 < radius within 2^+-50),
     // 2^-100 < |r| < 2^100 and |r - radius| > 2^-40 radius (so |a| > 2^-42), every operand
-    // and quotient of the five divisions is within 2^+-600.
-    const bool div_ok = S.div_fast && (fabs(r) > 0x1p-100) & (fabs(r) < 0x1p100) &
-                        (fabs(r - radius) > radius * 0x1p-40);
-    with_sincos<GRT_FAST_DIV>(theta, S.div_share, body, div_ok);
+    // and quotient of the five divisions is within 2^+-600 (schw_div_ok; device check of the
+    // two forms at the predicate's edges: tests/test_gpu_arith.py
+    // ::test_rhs_schwarzschild_fast_form_matches_ieee).
+    if constexpr (MODE != 0) {
+      double st, ct;
+      if (glibc::sincos_b_table_ok(theta)) glibc::sincos_b_table(theta, &st, &ct);
+      else glibc::sincos_b_taylor(theta, &st, &ct);
+      if constexpr (MODE == 1) body(st, ct, true, std::true_type{});
+      else body(st, ct, true, std::false_type{});
+      return;
+    }
+    with_sincos<GRT_FAST_DIV>(theta, S.div_share, body, schw_div_ok(S, r));
   } else if constexpr (G == GRT_GEOM_EUCLIDEAN_SPHERICAL) {  // euclidean_spherical.rs:48-70
     double r = y[1], theta = y[2];
     double v_t = y[4], v_r = y[5], v_theta = y[6], v_phi = y[7];
@@ -640,10 +705,17 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     // Divisions without range steps (div_inrange) in region B: there sin theta >= 0.75 and
     // 2^-55 < |cos theta| < 0.66, and with S.div_fast (radius, |a| within 2^+-50),
     // 2^-200 < |l_z| < 2^100, |r| < 2^100 and del within 2^+-300, every operand and
-    // quotient of the four divisions is within 2^+-600.
-    const bool div_ok = S.div_fast && (fabs(r) < 0x1p100) & in_div_range(del) & (fabs(l_z) > 0x1p-200) &
-                        (fabs(l_z) < 0x1p100);
-    with_sincos<GRT_FAST_DIV_BL>(theta, true, body, div_ok);
+    // quotient of the four divisions is within 2^+-600 (bl_div_ok; device check:
+    // tests/test_gpu_arith.py::test_rhs_kerr_bl_fast_form_matches_ieee).
+    if constexpr (MODE != 0) {
+      double st, ct;
+      if (glibc::sincos_b_table_ok(theta)) glibc::sincos_b_table(theta, &st, &ct);
+      else glibc::sincos_b_taylor(theta, &st, &ct);
+      if constexpr (MODE == 1) body(st, ct, true, std::true_type{});
+      else body(st, ct, true, std::false_type{});
+      return;
+    }
+    with_sincos<GRT_FAST_DIV_BL>(theta, true, body, bl_div_ok(S, r, del, l_z));
   } else if constexpr (G == GRT_GEOM_KERR) {  // kerr.rs:200-241
     double radius = S.radius, a = S.a;
     double x = y[1], yy = y[2], z = y[3];
@@ -663,13 +735,24 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
       o[6] = ks_accel<FD>(radius, a, 2, x, yy, z, Gc, p);
       o[7] = ks_accel<FD>(radius, a, 3, x, yy, z, Gc, p);
     };
+    if constexpr (MODE != 0) {
+      if constexpr (MODE == 1) body(std::true_type{});
+      else body(std::false_type{});
+      return;
+    }
 #if GRT_FAST_DIV_KS
     // The metric quotients without v_div_scale (div_fx) when every lane's state passes
     // ks_fd_ok (wave-uniform, like the region-B forms above)
-    if (S.div_fast && __ballot(!ks_fd_ok(a, x, yy, z)) == 0) {
+    if (S.div_fast && __ballot(!ks_fd_ok(a, x, yy, z, S.ks_cap)) == 0) {
+#if GRT_KS_PATH_COUNT
+      ks_path_count(0);
+#endif
       body(std::true_type{});
       return;
     }
+#endif
+#if GRT_KS_PATH_COUNT
+    ks_path_count(1);
 #endif
     body(std::false_type{});
   } else {  // Euclidean, euclidean.rs:47-53
@@ -1803,9 +1886,8 @@ struct LoopState {
   uint32_t nrec;
   int retries;
   bool c_valid;
-  double obs;  // observer energy (redshift.rs:40-43), for the final-state record
 };
-// Entry e of an entry arena `st` of m entries ([17][m] words: TailList::st).
+// Entry e of an entry arena `st` of m entries ([16][m] words: TailList::st).
 GDEV void tail_save(unsigned long long* st, uint64_t m, uint64_t e, const LoopState& s) {
   unsigned long long* w = st + e;
 #pragma unroll
@@ -1818,7 +1900,6 @@ GDEV void tail_save(unsigned long long* st, uint64_t m, uint64_t e, const LoopSt
   w[14 * m] = s.idx;
   w[15 * m] = (unsigned long long)s.nrec | ((unsigned long long)(uint32_t)s.retries << 32) |
               ((unsigned long long)(s.c_valid ? 1 : 0) << 48);
-  w[16 * m] = (unsigned long long)__double_as_longlong(s.obs);
 }
 GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopState& s) {
   const unsigned long long* w = st + e;
@@ -1834,7 +1915,6 @@ GDEV void tail_load(const unsigned long long* st, uint64_t m, uint64_t e, LoopSt
   s.nrec = (uint32_t)f;
   s.retries = (int)((f >> 32) & 0xffffu);
   s.c_valid = ((f >> 48) & 1u) != 0;
-  s.obs = __longlong_as_double((long long)w[16 * m]);
 }
 GDEV unsigned long long load_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1858,6 +1938,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   // items present: the capacity, or the count the adaptive pass decided on the device
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
   if (n_items == 0) return;  // an empty chunk of a supersample pass
+#if GRT_KS_PATH_COUNT
+  if (threadIdx.x < 4) ks_path_lds[threadIdx.x] = 0;  // ordered before use by the tables' barrier
+#endif
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -2028,7 +2111,6 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
                 s.nrec = nrec;
                 s.retries = retries;
                 s.c_valid = c_valid;
-                s.obs = rc.obs;
                 tail_save(tl.st, tl.cap, e, s);
                 RAY_TIME(n, idx, 1, __builtin_amdgcn_s_memrealtime());
                 RAY_TIME(n, idx, 4, ray_att);
@@ -2120,6 +2202,10 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     atomicAdd(stats + 1, (unsigned long long)w_att);
     atomicAdd(stats + 2, (unsigned long long)w_rays);
   }
+#if GRT_KS_PATH_COUNT
+  __syncthreads();  // every wave of the block has left its loop
+  if (threadIdx.x < 4) atomicAdd(&g_ks_path[threadIdx.x], ks_path_lds[threadIdx.x]);
+#endif
 }
 
 // ============================================================= tail kernel =======
@@ -2197,7 +2283,7 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
           done = true;
         } else {
           tail_load(tl.st, tl.cap, e, s);
-          rc.obs = s.obs;  // Kerr-Schild: the RHS and the momentum read no ray constant
+          rc.obs = 0.0;  // Kerr-Schild: the RHS, the momentum and fin_put read no ray constant
           rc.e = 0.0;
           rc.lz = 0.0;
           rc.q = 0.0;
@@ -2294,10 +2380,81 @@ __global__ void __launch_bounds__(64) trajectory_kernel(const DevScene* __restri
   tl.status[r] = (uint8_t)status;
 }
 
-hipError_t launch_div_check(uint64_t n, uint64_t seed, unsigned long long* d_counts, hipStream_t stream) {
-  hipLaunchKernelGGL(div_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, seed, d_counts);
+hipError_t launch_arith_map(uint32_t samples, uint64_t seed, uint8_t* d_map, uint8_t* d_zmap, uint8_t* d_smap,
+                            hipStream_t stream) {
+  hipLaunchKernelGGL(arith_map_kernel, dim3((2047u * 2047u + 255u) / 256u), dim3(256), 0, stream, samples, seed, d_map,
+                     d_zmap, d_smap);
   return hipGetLastError();
 }
+
+// Device check of the range-free RHS forms (tests/test_gpu_parity.py
+// ::test_rhs_fast_forms_match_ieee): for state i (y[8]; KerrBL: e, l_z, q in consts[3 i ..])
+// out[16 i ..] = the range-free form (rhs MODE 1), out[16 i + 8 ..] = the IEEE form (MODE 2),
+// pred[i] = whether the render's predicate admits the range-free form there.
+template <int G>
+__global__ void __launch_bounds__(64) rhs_check_kernel(const DevScene* __restrict__ Sp, const double* __restrict__ states,
+                                                      const double* __restrict__ consts, uint64_t n, double* out,
+                                                      uint8_t* pred) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();  // whole block, before the early return
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  double y[8], of[8], oi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) y[k] = states[8 * i + k];
+  RayConst rc{};
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    rc.e = consts[3 * i];
+    rc.lz = consts[3 * i + 1];
+    rc.q = consts[3 * i + 2];
+  }
+  rhs<G, 1>(S, rc, y, of);
+  rhs<G, 2>(S, rc, y, oi);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    out[16 * i + k] = of[k];
+    out[16 * i + 8 + k] = oi[k];
+  }
+  bool p = false;
+  const bool region_b = glibc::sincos_b_table_ok(y[2]) || glibc::sincos_b_taylor_ok(y[2]);
+  if constexpr (G == GRT_GEOM_SCHWARZSCHILD) p = S.div_share && region_b && schw_div_ok(S, y[1]);
+  if constexpr (G == GRT_GEOM_KERR_BL) p = region_b && bl_div_ok(S, y[1], bl_delta(y[1], S.radius, S.a), rc.lz);
+  if constexpr (G == GRT_GEOM_KERR) p = S.div_fast && ks_fd_ok(S.a, y[1], y[2], y[3], S.ks_cap);
+  pred[i] = p ? 1 : 0;
+}
+
+hipError_t launch_rhs_check(int geometry, const DevScene* d_scene, const double* d_states, const double* d_consts,
+                            uint64_t n, double* d_out, uint8_t* d_pred, hipStream_t stream) {
+  const unsigned blocks = (unsigned)((n + 63) / 64);
+  switch (geometry) {
+    case GRT_GEOM_SCHWARZSCHILD:
+      hipLaunchKernelGGL(rhs_check_kernel<GRT_GEOM_SCHWARZSCHILD>, dim3(blocks), dim3(64), 0, stream, d_scene, d_states,
+                         d_consts, n, d_out, d_pred);
+      break;
+    case GRT_GEOM_KERR:
+      hipLaunchKernelGGL(rhs_check_kernel<GRT_GEOM_KERR>, dim3(blocks), dim3(64), 0, stream, d_scene, d_states, d_consts,
+                         n, d_out, d_pred);
+      break;
+    case GRT_GEOM_KERR_BL:
+      hipLaunchKernelGGL(rhs_check_kernel<GRT_GEOM_KERR_BL>, dim3(blocks), dim3(64), 0, stream, d_scene, d_states,
+                         d_consts, n, d_out, d_pred);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+#if GRT_KS_PATH_COUNT
+hipError_t ks_path_read(unsigned long long* out, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ks_path), sizeof(g_ks_path));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_ks_path), z, sizeof(z));
+  }
+  return e;
+}
+#endif
 
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream) {
   if (tl.n == 0) return hipSuccess;

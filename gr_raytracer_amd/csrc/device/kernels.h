@@ -47,7 +47,13 @@ struct TrajectoryList {
   uint8_t* status;
 };
 // test hook: div_inrange / div2_inrange against the compiler's division on n random pairs
-hipError_t launch_div_check(uint64_t n, uint64_t seed, unsigned long long* d_counts, hipStream_t stream);
+hipError_t launch_arith_map(uint32_t samples, uint64_t seed, uint8_t* d_map, uint8_t* d_zmap, uint8_t* d_smap,
+                            hipStream_t stream);
+hipError_t launch_rhs_check(int geometry, const DevScene* d_scene, const double* d_states, const double* d_consts,
+                            uint64_t n, double* d_out, uint8_t* d_pred, hipStream_t stream);
+#if GRT_KS_PATH_COUNT
+hipError_t ks_path_read(unsigned long long* out, bool reset);
+#endif
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
 
 // Invariant monitors of the n = rows x cols rays of a rectangle (health_kernel):

@@ -26,6 +26,9 @@ RENDER_FLAGS = ("--filename", "--from-row", "--from-col", "--to-row", "--to-col"
 
 
 # Debug names of the RaytracerError variants a pixel can end in (grt_main.cpp's table)
+# exit status of a frame written with pixels that lost hit candidates (the device hit pool
+# could not hold them after two reserves): the image is incomplete
+EXIT_INCOMPLETE = 3
 ERROR_NAMES = {1: "IntegrationError(MaxStepsReached)", 2: "NoCircularOrbitPossible", 3: "BelowRISCO",
                4: "NonFiniteRadius"}
 
@@ -163,6 +166,7 @@ def main(argv=None) -> int:
         supersampled = bool(cfg.enabled) or mask is not None
         if supersampled and rank == 0:  # raytracer.rs:264-267
             _log(f"[render_dist] INFO Rendering section from (0, 0) to ({scene.rows}, {scene.cols}) with supersampling")
+        incomplete = 0  # pixels still missing hit candidates after the last trace
         for attempt in range(3):
             fails = L.SubsampleFailures(fail_cap, L.ptr(f_pix, C.c_uint32), L.ptr(f_smp, C.c_uint32),
                                         L.ptr(f_st, C.c_uint8), 0, L.ptr(f_stop, C.c_uint8), L.ptr(f_steps, C.c_uint32))
@@ -179,10 +183,11 @@ def main(argv=None) -> int:
             if int(lost[0]) == 0:
                 break
             if attempt == 2:  # the pool cannot hold them (2^31 records): the frame is incomplete
+                incomplete = int(lost[0])
                 if rank == 0:
-                    _log(f"[render_dist] ERROR {int(lost[0])} pixels lost hit candidates after growing the device "
+                    _log(f"[render_dist] ERROR {incomplete} pixels lost hit candidates after growing the device "
                           "hit pool twice; they are written without their candidates past the first "
-                          f"{L.GRT_MAX_HITS}")
+                          f"{L.GRT_MAX_HITS}, and the exit status is {EXIT_INCOMPLETE}")
                 break
             if rank == 0:
                 _log(f"[render_dist] WARN {int(lost[0])} pixels lost hit candidates (device hit pool full); "
@@ -222,7 +227,7 @@ def main(argv=None) -> int:
             dist.all_reduce(stats)
             totals = stats.cpu()
         if rank != 0:
-            return 0
+            return EXIT_INCOMPLETE if incomplete else 0
         w, h = scene.cols, scene.rows
         if want_f64:
             xyza64, _cls, _status, n_sel = out
@@ -246,7 +251,7 @@ def main(argv=None) -> int:
               f"{n_sel} supersampled pixels, frame {t_render:.3f} s ({steps / t_render:.3e} steps/s)")
         _log(f"[render_dist] INFO saved image to {a.filename}")  # raytracer.rs:494, main.rs:175-176
         _log(f"[render_dist] INFO Elapsed time: {duration_debug_2(time.perf_counter() - t_start)}")
-        return 0
+        return EXIT_INCOMPLETE if incomplete else 0
     finally:
         dist.destroy_process_group()
 

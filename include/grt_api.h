@@ -351,6 +351,10 @@ int grt_scene_create(const grt_scene_desc* desc, grt_scene** out);
 int grt_scene_destroy(grt_scene* scene);
 const char* grt_last_error(void);
 int grt_device_count(void);
+/* SHA-256 (64 hex digits) of the sources this library was built from
+ * (gr_raytracer_amd/source_hash.py; "unstamped" for a copy built outside the checkout).
+ * No reference counterpart: it ties a prebuilt library to its checkout. */
+const char* grt_source_hash(void);
 
 /* Trace a rows x cols rectangle at 1 spp (or the offset list) on `device`.
  * Host output arrays, row-major over the rectangle (or per offset entry). */

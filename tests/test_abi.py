@@ -65,3 +65,28 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "LIB_PATH", tmp_path / "nope.so")
     with pytest.raises(L.GrtError):
         L.lib()
+
+
+def test_library_from_other_sources_is_refused(grt, tmp_path):
+    """The source stamp (grt_source_hash, Makefile) binds libgrt.so to its checkout: a
+    library whose stamp differs from the checkout's source hash raises GrtError."""
+    import os
+    import sys
+
+    from gr_raytracer_amd import _lib as L
+    from gr_raytracer_amd.source_hash import source_hash
+
+    want = source_hash()
+    assert L.lib().grt_source_hash().decode() == want  # this build matches its checkout
+    data = L.LIB_PATH.read_bytes()
+    assert data.count(want.encode()) == 1
+    other = ("0" if want[0] != "0" else "1") + want[1:]
+    patched = tmp_path / "libgrt.so"
+    patched.write_bytes(data.replace(want.encode(), other.encode()))
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); from gr_raytracer_amd import _lib as L\n"
+            "try:\n    L.lib()\nexcept L.GrtError as e:\n    print('refused:', e); sys.exit(3)\nsys.exit(0)")
+    env = {k: v for k, v in os.environ.items() if k != "GRT_LIB_ALLOW_MISSING"}
+    env["GRT_LIB"] = str(patched)
+    r = subprocess.run([sys.executable, "-c", code, str(ROOT)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 3, r.stdout + r.stderr
+    assert "built from other sources" in r.stdout

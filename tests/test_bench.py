@@ -1,4 +1,5 @@
-"""bench.py's host logic on CPU: the C4 strong-scaling loop over gloo (world 2), the
+"""bench.py's host logic on CPU: the C4 strong-scaling loop over gloo (world 2, and world 8
+with 16-row cyclic bands: the north-star layout), the
 host-core census, and the roofline's refusal of a PMC summary from another build.
 
 The C4 loop (bench.c4_frame_steps / c4_summary) is backend-agnostic; here each rank's
@@ -25,15 +26,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _opts(g):
+def _opts(g, rows=SIZE, cols=SIZE):
     import bench
 
     o = bench.c4_opts(g, SIZE, max_steps=3000)
     o.max_radius = 100.0
+    o.height, o.width = rows, cols
     return o
 
 
-def _worker(rank, world, port, band_rows, out_dir):
+def _worker(rank, world, port, band_rows, out_dir, rows=SIZE, cols=SIZE):
     import sys
     import time
 
@@ -52,17 +54,17 @@ def _worker(rank, world, port, band_rows, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        hs = host_scene(g, "kerr.toml", _opts(g))
-        rows = shard_frame_rows(SIZE, band_rows, rank, world)
+        hs = host_scene(g, "kerr.toml", _opts(g, rows, cols))
+        mine = shard_frame_rows(rows, band_rows, rank, world)
 
         def trace_shard():
             t0 = time.perf_counter()
-            r = O.render_pixels(hs.desc, 0, 0, SIZE, SIZE, threads=2, row_list=rows)
+            r = O.render_pixels(hs.desc, 0, 0, rows, cols, threads=1 if world > 4 else 2, row_list=mine)
             rec = pack_records(torch.from_numpy(r["xyza"].astype(np.float32)), torch.from_numpy(r["ray_class"]),
                                torch.from_numpy(r["status"]))
             return rec, float(r["accepted"]), float(r["attempts"]), (time.perf_counter() - t0) * 1e3
 
-        res = bench.c4_frame_steps(trace_shard, rank, world, SIZE, SIZE, band_rows, steps=2, warmup=1,
+        res = bench.c4_frame_steps(trace_shard, rank, world, rows, cols, band_rows, steps=2, warmup=1,
                                    sync=lambda: None)
         s = bench.c4_summary(res, rank, world)
         if rank == 0:
@@ -77,27 +79,34 @@ def _worker(rank, world, port, band_rows, out_dir):
         dist.destroy_process_group()
 
 
-def test_c4_strong_scaling_loop_gloo_world2(grt, oracle):
+# world 8, 16-row bands: the north-star layout; 136 rows = one band per rank plus a ragged
+# ninth band (rank 0), on a narrow frame so the oracle's Kerr-Schild traces stay short
+@pytest.mark.parametrize("world,band_rows,rows,cols", [(2, 4, SIZE, SIZE), (8, 16, 136, 6)])
+def test_c4_strong_scaling_loop_gloo(grt, oracle, world, band_rows, rows, cols):
     import torch.multiprocessing as mp
 
-    from gr_raytracer_amd.distributed import pack_records
+    from gr_raytracer_amd.distributed import pack_records, shard_frame_rows, shard_row_count
 
     import torch
 
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), 4, d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), band_rows, d, rows, cols), nprocs=world, join=True)
         frame = np.load(os.path.join(d, "frame.npy"))
         s = json.load(open(os.path.join(d, "summary.json")))
-    hs = host_scene(grt, "kerr.toml", _opts(grt))
-    ref = oracle.render_pixels(hs.desc, 0, 0, SIZE, SIZE, threads=4)
+    hs = host_scene(grt, "kerr.toml", _opts(grt, rows, cols))
+    ref = oracle.render_pixels(hs.desc, 0, 0, rows, cols, threads=4)
     want = pack_records(torch.from_numpy(ref["xyza"].astype(np.float32)), torch.from_numpy(ref["ray_class"]),
                         torch.from_numpy(ref["status"])).numpy()
     assert np.array_equal(frame, want)
-    assert len(s["per_rank_kernel_ms"]) == 2 and all(v > 0 for v in s["per_rank_kernel_ms"])
+    assert all(shard_row_count(rows, band_rows, k, world) > 0 for k in range(world))
+    assert len(s["per_rank_kernel_ms"]) == world and all(v > 0 for v in s["per_rank_kernel_ms"])
     assert s["imbalance"] >= 1.0
     assert s["gather_ms"] > 0
     assert s["steps"] == 2
     assert s["accepted"] == 2 * ref["accepted"]  # two frames, every rank's steps
+    # rank 0's own share: its bands' accepted steps, two frames
+    steps = ref["steps"].reshape(rows, cols).astype(np.int64)
+    assert s["rank0_accepted"] == 2 * steps[shard_frame_rows(rows, band_rows, 0, world)].sum()
 
 
 def test_host_cores_census():

@@ -1,4 +1,4 @@
-"""Multi-rank frame assembly on CPU (gloo, world_size 2 and 3).
+"""Multi-rank frame assembly on CPU (gloo, world_size 2, 3 and 8).
 
 Each rank renders its cyclic row-band shard (here with the oracle as a stand-in for
 the GPU trace, since this container has no GPU), packs 18-byte pixel records and
@@ -25,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, band_rows, out_dir):
+def _worker(rank, world, port, band_rows, out_dir, frame_rows=FRAME_ROWS, frame_cols=FRAME_COLS):
     import sys
 
     sys.path.insert(0, str(ROOT))
@@ -42,12 +42,12 @@ def _worker(rank, world, port, band_rows, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        hs = host_scene(g, "schwarzschild.toml", c2_opts(g, width=FRAME_COLS, height=FRAME_ROWS))
-        rows = shard_frame_rows(FRAME_ROWS, band_rows, rank, world)
-        r = O.render_pixels(hs.desc, 0, 0, FRAME_ROWS, FRAME_COLS, threads=2, row_list=rows)
+        hs = host_scene(g, "schwarzschild.toml", c2_opts(g, width=frame_cols, height=frame_rows))
+        rows = shard_frame_rows(frame_rows, band_rows, rank, world)
+        r = O.render_pixels(hs.desc, 0, 0, frame_rows, frame_cols, threads=1 if world > 4 else 2, row_list=rows)
         xyza = torch.from_numpy(r["xyza"].astype(np.float32))
         rec = pack_records(xyza, torch.from_numpy(r["ray_class"]), torch.from_numpy(r["status"]))
-        frame = gather_frame(rec, FRAME_ROWS, FRAME_COLS, band_rows, rank, world)
+        frame = gather_frame(rec, frame_rows, frame_cols, band_rows, rank, world)
         if rank == 0:
             fx, fc, fs = unpack_records(frame)
             np.savez(os.path.join(out_dir, "frame.npz"), xyza=fx.numpy(), cls=fc.numpy(), status=fs.numpy())
@@ -57,15 +57,18 @@ def _worker(rank, world, port, band_rows, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,band_rows", [(2, 8), (3, 16)])
-def test_gloo_sharded_frame_equals_single_process(oracle, grt, world, band_rows):
+# world 8 with 16-row bands is the north-star layout (8 ranks, cyclic 16-row bands): 136
+# rows give every rank one whole band and a ragged ninth band (8 rows) to rank 0
+@pytest.mark.parametrize("world,band_rows,frame_rows,frame_cols", [(2, 8, 40, 36), (3, 16, 40, 36),
+                                                                    (8, 16, 136, 10)])
+def test_gloo_sharded_frame_equals_single_process(oracle, grt, world, band_rows, frame_rows, frame_cols):
     import torch.multiprocessing as mp
 
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), band_rows, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), band_rows, d, frame_rows, frame_cols), nprocs=world, join=True)
         got = np.load(os.path.join(d, "frame.npz"))
-        hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=FRAME_COLS, height=FRAME_ROWS))
-        ref = oracle.render_pixels(hs.desc, 0, 0, FRAME_ROWS, FRAME_COLS, threads=4)
+        hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=frame_cols, height=frame_rows))
+        ref = oracle.render_pixels(hs.desc, 0, 0, frame_rows, frame_cols, threads=4)
         assert np.array_equal(got["xyza"], ref["xyza"].astype(np.float32))
         assert np.array_equal(got["cls"], ref["ray_class"])
         assert np.array_equal(got["status"], ref["status"])

@@ -369,21 +369,3 @@ def test_row_shards_reassemble_the_frame(grt, gpu, n_shards, band_rows):
         rows = shard_frame_rows(100, band_rows, s, n_shards)
         assert np.array_equal(part.xyza64.reshape(len(rows), 120, 4), f64[rows])
         assert np.array_equal(part.steps.reshape(len(rows), 120), steps[rows])
-
-
-def test_division_in_range(grt):
-    """The range-free divisions (geodesic.hip div_inrange / div2_inrange: the compiler's
-    f64 division expansion without its range steps, used by the region-B RHS; div_fx:
-    without v_div_scale but with v_div_fixup, used by the Kerr-Schild RHS) return the
-    compiler's division bits on 2 x 16M random operand pairs with |x|, |y| in
-    2^-300 .. 2^300 (div_fx also with signed-zero numerators)."""
-    import ctypes as C
-
-    lib = grt.lib()
-    fn = lib.grt_debug_div_check
-    fn.restype = C.c_int
-    fn.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
-    for seed in (1, 0x9E3779B97F4A7C15):
-        bad = C.c_uint64(1)
-        assert fn(0, 1 << 24, seed, C.byref(bad)) == 0
-        assert bad.value == 0
