@@ -574,7 +574,14 @@ int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList*
 // geodesic.hip), one process-wide buffer (single-device diagnostics).
 unsigned long long* g_rt = nullptr;
 uint64_t g_rt_cap = 0, g_rt_n = 0;
+uint64_t g_rt_trace = 0, g_rt_only = 0;  // record only trace g_rt_only since grt_debug_ray_times_only (0: each)
 int ray_times_reserve(uint64_t n, hipStream_t stream) {
+  ++g_rt_trace;
+  if (g_rt_only && g_rt_trace != g_rt_only) {  // another trace: it records nothing
+    HIP_TRY(hipDeviceSynchronize());          // the recorded kernel may still be running
+    HIP_TRY(grt::set_ray_times(nullptr));
+    return 0;
+  }
   if (n > g_rt_cap) {
     if (g_rt) {
       (void)hipDeviceSynchronize();
@@ -764,6 +771,14 @@ int grt_debug_probe_order(grt_scene* s, int device, const grt_row_shard* sh, uin
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(probe_out, dc->sched_mem, n_tiles * 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(order_out, order, n_tiles * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// Diagnostic builds only (not in grt_api.h): record the schedule of the k-th trace from
+// now on (and of no other), or of every trace (k = 0): C5's supersample chunk is trace 2.
+int grt_debug_ray_times_only(uint64_t k) {
+  g_rt_only = k;
+  g_rt_trace = 0;
   return 0;
 }
 

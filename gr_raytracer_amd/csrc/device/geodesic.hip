@@ -12,7 +12,7 @@
 // visits exactly the same windows in the same order, so no trajectory ever leaves
 // the register file.
 //
-// The grid is persistent: each wave pulls 64-item chunks of work from one global
+// The grid is persistent: each wave claims exactly the items it starts from one global
 // counter, and whenever lanes finish their ray a wave ballot hands them the next
 // items (lane refill), so long (near-photon-sphere) and short (captured) rays never
 // leave lanes idle until the queue is empty.
@@ -1121,6 +1121,39 @@ GDEV void momentum(const DevScene& S, const RayConst& rc, const double* y, doubl
   }
 }
 
+// x unchanged, through an empty volatile asm: the compiler can neither hoist what is
+// computed from the result out of the branch it sits in nor merge it with the same
+// computation on x elsewhere.
+GDEV double opaque(double x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// The window pass's lerped momentum of a hit, sw p(ya) + t p(yb) (objects.rs:27-44).
+// KerrBL reads the momentum's inputs through opaque(): otherwise both momenta, invariant
+// in the object loop, have their sincos-free parts computed before the loop for every
+// near-field window and kept live across it, and the 3-wave kernel spills them (the
+// scratch stores of C3: 1.75 GB written per frame).  Now they are computed only for a
+// recorded hit (1.55M of 1.79e9 C3 steps), with the same operations on the same values.
+// (An out-of-line function does the same for the spills, but the call makes the kernel
+// rematerialise its SGPR constants around it: +20% scalar instructions, +1.5% time.)
+template <int G>
+GDEV void lerp_momentum(const DevScene& S, const RayConst& rc, const double* ya, const double* yb, double t,
+                        double* ph) {
+  double pa[4], pb[4];
+  if constexpr (G == GRT_GEOM_KERR_BL) {
+    const double a8[8] = {0.0, opaque(ya[1]), opaque(ya[2]), 0.0, opaque(ya[4]), opaque(ya[5]), 0.0, 0.0};
+    const double b8[8] = {0.0, opaque(yb[1]), opaque(yb[2]), 0.0, opaque(yb[4]), opaque(yb[5]), 0.0, 0.0};
+    momentum<G>(S, rc, a8, pa);
+    momentum<G>(S, rc, b8, pb);
+  } else {
+    momentum<G>(S, rc, ya, pa);
+    momentum<G>(S, rc, yb, pb);
+  }
+  const double sw = 1.0 - t;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ph[q] = sw * pa[q] + t * pb[q];
+}
+
 // inner_product at a native-chart point whose polar-angle sin/cos are given.
 template <int G>
 GDEV double inner(const DevScene& S, const double* pos, double st, double ct, const double* v,
@@ -1842,15 +1875,13 @@ GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc
       double distance = sqrt(dx * dx + dy * dy + dz * dz);
       if (!(distance < shortest)) continue;
       shortest = distance;
+      double ph[4];
+      if (writer) lerp_momentum<G>(S, rc, y, yn, t, ph);
       if (writer && nrec < GRT_WS_SLOTS) {
-        double pa[4], pb[4];
-        momentum<G>(S, rc, y, pa);
-        momentum<G>(S, rc, yn, pb);
-        double sw = 1.0 - t;
         const uint64_t slot = (uint64_t)nrec * n + idx;
         double2* d = reinterpret_cast<double2*>(ws.rec + slot);
-        d[0] = make_double2(sw * pa[0] + t * pb[0], sw * pa[1] + t * pb[1]);
-        d[1] = make_double2(sw * pa[2] + t * pb[2], sw * pa[3] + t * pb[3]);
+        d[0] = make_double2(ph[0], ph[1]);
+        d[1] = make_double2(ph[2], ph[3]);
         d[2] = make_double2(pt[0], pt[1]);
         d[3] = make_double2(pt[2], __hiloint2double((int)k, (int)(uint32_t)i));
         if constexpr (VOL) {  // chord direction for the raymarch (volumetric_disc.rs:576, :589-594)
@@ -1859,12 +1890,6 @@ GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc
           ws.rec_dir[(uint64_t)2 * GRT_WS_SLOTS * n + slot] = cn[2] - c[2];
         }
       } else if (writer) {  // beyond the workspace slots: the hit pool
-        double pa[4], pb[4], ph[4];
-        momentum<G>(S, rc, y, pa);
-        momentum<G>(S, rc, yn, pb);
-        double sw = 1.0 - t;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ph[q] = sw * pa[q] + t * pb[q];
         double dir[3] = {cn[0] - c[0], cn[1] - c[1], cn[2] - c[2]};
         hit_append(ws, idx, nrec, (uint32_t)i, k, ph, pt, VOL ? dir : nullptr);
       }
@@ -1944,7 +1969,6 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  constexpr uint64_t CHUNK = 64;
   const uint64_t n = ws.n;
   constexpr bool TAIL = (G == GRT_GEOM_KERR);
   const bool tail_on = TAIL && tl.cap != 0;
@@ -1986,7 +2010,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
 #endif
 
   while (true) {
-    // ---------------- lane refill: ballot, one atomic per 64 items --------------
+    // ---------------- lane refill: ballot, one atomic per refill ----------------
     bool need = !active && !done;
     uint64_t need_mask = __ballot(need);
     if (need_mask) {
@@ -1994,12 +2018,13 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       uint64_t cnt = __popcll(need_mask);
       uint64_t remaining = chunk_end - chunk_next;
       uint64_t new_base = 0;
-      // Kerr-Schild claims exactly the items it starts now: a wave whose lanes are all busy
-      // with 1e6-step rays must not sit on unstarted items of a 64-item chunk (they would
-      // start only when one of its lanes frees up, possibly after the whole queue ran).
-      // Its rays are long, so the extra atomics are rare.
-      // A two-ended queue's claims are exact as well (remaining stays 0).
-      const uint64_t take = (TAIL || two_ended) ? cnt - remaining : CHUNK;
+      // Claims are exact: a wave takes exactly the items it starts now.  A wave holding
+      // unstarted items of a larger chunk when the queue drains starts them one ray
+      // lifetime late, on its own lanes, while other waves have emptied (Kerr-Schild's
+      // 1e6-step rays first; then C5's supersample pass, ~2.5 sub-rays per lane: its
+      // last ray started at 0.375 s of a 0.47 s pass with 64-item chunks, at 0.21 s of
+      // 0.39 s with exact claims; C2 -2.5%; profiles/r05d, r05e).  One atomic per refill.
+      const uint64_t take = cnt - remaining;
       if (cnt > remaining) {
         unsigned long long b = 0;
         if (lane == 0) b = atomicAdd(counter, from_back ? (unsigned long long)take << 32 : (unsigned long long)take);
