@@ -73,12 +73,16 @@ def cat(op, loc):
 
 
 # the RHS: sincos and at least three reciprocals (five divisions, two sharing one)
-best = max((b for b in blocks if any(cat(o, l) == "sincos" for o, l in b["ins"]) and
-            sum(o.startswith("v_rcp_f64") for o, _ in b["ins"]) >= 3), key=lambda b: len(b["ins"]))
-c = collections.Counter(cat(o, l) for o, l in best["ins"])
-valu = sum(v for k, v in c.items() if k in ("division", "sincos", "f64", "other"))
-print(f"integrate_kernel<{G}, false> {best['name']}: {len(best['ins'])} instructions, {valu} VALU")
-for k in ("f64", "division", "sincos", "other", "salu", "lds", "mem"):
-    print(f"  {k:9s} {c.get(k, 0):4d}" + (f"  ({c.get(k, 0) / valu:.0%} of VALU)" if k in ("f64", "division", "sincos", "other") else ""))
-ops = collections.Counter(o for o, l in best["ins"] if cat(o, l) in ("division",))
-print("  division ops:", dict(ops))
+# with ALL=1: every such block (the region-B forms: table / Taylor sincos, with the IEEE
+# or the range-free divisions), largest first
+import os  # noqa: E402
+cands = sorted((b for b in blocks if any(cat(o, l) == "sincos" for o, l in b["ins"]) and
+                sum(o.startswith("v_rcp_f64") for o, _ in b["ins"]) >= 3), key=lambda b: -len(b["ins"]))
+for best in (cands if os.environ.get("ALL") == "1" else cands[:1]):
+    c = collections.Counter(cat(o, l) for o, l in best["ins"])
+    valu = sum(v for k, v in c.items() if k in ("division", "sincos", "f64", "other"))
+    print(f"integrate_kernel<{G}, false> {best['name']}: {len(best['ins'])} instructions, {valu} VALU")
+    for k in ("f64", "division", "sincos", "other", "salu", "lds", "mem"):
+        print(f"  {k:9s} {c.get(k, 0):4d}" + (f"  ({c.get(k, 0) / valu:.0%} of VALU)" if k in ("f64", "division", "sincos", "other") else ""))
+    ops = collections.Counter(o for o, l in best["ins"] if cat(o, l) in ("division",))
+    print("  division ops:", dict(ops))
