@@ -70,6 +70,9 @@ namespace grt {
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
+#ifndef GRT_TAIL_PRIO
+#define GRT_TAIL_PRIO 1  // light charts: issue priority by steps left once the queue drains (C5 -1.2%, profiles/r05i)
+#endif
 #ifndef GRT_RAY_TIMES
 #define GRT_RAY_TIMES 0  // diagnostic builds only: per-ray schedule record (tools/c4_ray_times.py)
 #endif
@@ -2092,6 +2095,24 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         }
       }
       w_rays += __popcll(__ballot(fresh));
+#if GRT_TAIL_PRIO
+      if constexpr (!TAIL) {
+        // After the queue has drained for this wave (one of its lanes found no item), the
+        // pass ends on the rays with the most steps left, so the waves holding them get the
+        // SIMD's issue slots first (s_setprio; the arbiter otherwise serves the oldest wave):
+        // the estimate of what is left is max_radius unit steps (a ray escapes after about
+        // that many) minus the wave's fewest accepted steps.  Scheduling only, never results.
+        if (!two_ended && __ballot(done) != 0) {
+          uint32_t mi = active ? (uint32_t)i : 0xffffffffu;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) mi = min(mi, (uint32_t)__shfl_xor((int)mi, off));
+          const double len = sqrt(S.max_radius_sq), left = len - (double)mi;
+          if (left > 0.67 * len) __builtin_amdgcn_s_setprio(3);
+          else if (left > 0.33 * len) __builtin_amdgcn_s_setprio(2);
+          else __builtin_amdgcn_s_setprio(1);
+        }
+      }
+#endif
       if (cnt > remaining) {
         chunk_next = new_base + (cnt - remaining);
         chunk_end = new_base + take;
