@@ -12,7 +12,7 @@
 // visits exactly the same windows in the same order, so no trajectory ever leaves
 // the register file.
 //
-// The grid is persistent: each wave claims exactly the items it starts from one global
+// The grid is persistent: each wave claims work items from one global
 // counter, and whenever lanes finish their ray a wave ballot hands them the next
 // items (lane refill), so long (near-photon-sphere) and short (captured) rays never
 // leave lanes idle until the queue is empty.
@@ -1972,6 +1972,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  constexpr uint64_t CHUNK = 64;
   const uint64_t n = ws.n;
   constexpr bool TAIL = (G == GRT_GEOM_KERR);
   const bool tail_on = TAIL && tl.cap != 0;
@@ -2013,7 +2014,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
 #endif
 
   while (true) {
-    // ---------------- lane refill: ballot, one atomic per refill ----------------
+    // ---------------- lane refill: ballot, one atomic per claim ------------------
     bool need = !active && !done;
     uint64_t need_mask = __ballot(need);
     if (need_mask) {
@@ -2022,12 +2023,17 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       uint64_t remaining = chunk_end - chunk_next;
       uint64_t new_base = 0;
       // Claims are exact: a wave takes exactly the items it starts now.  A wave holding
-      // unstarted items of a larger chunk when the queue drains starts them one ray
-      // lifetime late, on its own lanes, while other waves have emptied (Kerr-Schild's
-      // 1e6-step rays first; then C5's supersample pass, ~2.5 sub-rays per lane: its
-      // last ray started at 0.375 s of a 0.47 s pass with 64-item chunks, at 0.21 s of
-      // 0.39 s with exact claims; C2 -2.5%; profiles/r05d, r05e).  One atomic per refill.
-      const uint64_t take = cnt - remaining;
+      // unstarted items of a 64-item chunk when the queue drains starts them one ray
+      // lifetime late, on its own lanes, while other waves have emptied (C5's supersample
+      // pass, ~2.5 sub-rays per lane: its last ray started at 0.375 s of a 0.47 s pass with
+      // chunks, at 0.21 s of 0.39 s with exact claims; C2 -2.5%; profiles/r05d, r05e).
+      // KerrBL claims 64-item chunks until its view of the counter is within two grids'
+      // worth of lanes of the end: its 2.25M short rays end ~13M times a second, and an
+      // atomic on one address per refill cost C3 +16% (profiles/r05l, r05m).
+      const uint64_t grid_lanes = (uint64_t)gridDim.x * blockDim.x;
+      const bool exact =
+          TAIL || two_ended || G != GRT_GEOM_KERR_BL || chunk_end + 2 * grid_lanes >= n_items;
+      const uint64_t take = exact ? cnt - remaining : CHUNK;
       if (cnt > remaining) {
         unsigned long long b = 0;
         if (lane == 0) b = atomicAdd(counter, from_back ? (unsigned long long)take << 32 : (unsigned long long)take);
@@ -2096,7 +2102,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       }
       w_rays += __popcll(__ballot(fresh));
 #if GRT_TAIL_PRIO
-      if constexpr (!TAIL) {
+      if constexpr (!TAIL && G != GRT_GEOM_KERR_BL) {  // KerrBL's rays are all short
         // After the queue has drained for this wave (one of its lanes found no item), the
         // pass ends on the rays with the most steps left, so the waves holding them get the
         // SIMD's issue slots first (s_setprio; the arbiter otherwise serves the oldest wave):
