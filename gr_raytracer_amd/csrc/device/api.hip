@@ -25,6 +25,7 @@
 namespace {
 
 int g_blocks_per_cu = 0;
+int g_range_free = 1;  // grt_debug_range_free: 0 = every division and sqrt in its IEEE form (tests)
 int g_threads = 256;
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
 int g_two_ended = 1;  // grt_set_two_ended: probe-ordered traces take the queue from both ends
@@ -315,7 +316,8 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     const int lim = d.geometry == GRT_GEOM_KERR ? 20 : 50;
     const bool a_mod = std::fpclassify(d.a) == FP_NORMAL && ea > -lim && ea < lim;
     const bool a_ok = d.geometry == GRT_GEOM_KERR_BL ? a_mod : (d.geometry != GRT_GEOM_KERR || a_mod || d.a == 0.0);
-    ds.div_fast = (std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -lim && ex < lim && a_ok) ? 1 : 0;
+    ds.div_fast = (g_range_free && std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -lim && ex < lim &&
+                   a_ok) ? 1 : 0;
     // ks_fd_ok's coordinate bound: 2^ceil(log2(2 max_radius)) covers every state of a ray
     // (it stops one step beyond max_radius), within the proven 2^10 .. 2^32
     int em = 0;
@@ -847,15 +849,24 @@ int grt_debug_rhs_check(grt_scene* s, int device, uint64_t n, const double* stat
   return 0;
 }
 
-#if GRT_KS_PATH_COUNT
-// Diagnostic builds only (not in grt_api.h): rhs<KERR> evaluations by form since the last
-// reset: [0] wave-level range-free, [1] wave-level IEEE, [2] / [3] the same in lanes.
-int grt_debug_ks_path(uint64_t* out, int reset) {
+#if GRT_PATH_COUNT
+// Diagnostic builds only (not in grt_api.h): the integrate kernels' path counters since the
+// last reset (geodesic.hip path_count): out[16], [k] wave-level, [8 + k] lane-level.
+int grt_debug_path_counts(uint64_t* out, int reset) {
   if (!out) return fail(-EINVAL, "null argument");
-  HIP_TRY(grt::ks_path_read((unsigned long long*)out, reset != 0));
+  HIP_TRY(grt::path_read((unsigned long long*)out, reset != 0));
   return 0;
 }
 #endif
+
+// Test hook (not in grt_api.h): 0 makes the device copies of scenes created (first rendered)
+// afterwards run every division and square root of the RHS in the compiler's IEEE form
+// (DevScene::div_fast = 0), so a test can hold the range-free forms to them end to end.
+int grt_debug_range_free(int on) {
+  if (on != 0 && on != 1) return fail(-EINVAL, "range-free arithmetic: 0 or 1");
+  g_range_free = on;
+  return 0;
+}
 
 int grt_set_two_ended(int on) {
   if (on != 0 && on != 1) return fail(-EINVAL, "two-ended queue: 0 or 1");

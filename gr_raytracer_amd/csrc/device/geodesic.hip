@@ -495,6 +495,30 @@ GDEV void metric_bl(double r_s, double a, double r, double sin_t, double cos_t, 
   g[3][0] = g_tph;
 }
 
+#ifndef GRT_PATH_COUNT
+#define GRT_PATH_COUNT 0  // diagnostic builds only: count code paths per wave and per lane
+#endif
+#if GRT_PATH_COUNT
+// Diagnostic counters of integrate_kernel, [k] wave-level executions (one lane counts each),
+// [8 + k] the same in lanes.  Kerr-Schild RHS: 0 range-free form, 1 IEEE form.  Light
+// charts' RHS: 0 region-B table with range-free divisions, 1 region-B Taylor with them,
+// 2 region-B with the IEEE divisions, 3 general (branchy) sincos.  All: 4 near-field window
+// pass, 5 accepted step, 6 attempt.
+constexpr int NPATH = 8;
+__shared__ unsigned long long path_lds[2 * NPATH];
+__device__ unsigned long long g_path[2 * NPATH];
+GDEV void path_count(int k) {
+  const uint64_t m = __ballot(1);  // the lanes executing this path together
+  if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) {
+    atomicAdd(&path_lds[k], 1ull);
+    atomicAdd(&path_lds[NPATH + k], (unsigned long long)__popcll(m));
+  }
+}
+#define PATH_COUNT(k) path_count(k)
+#else
+#define PATH_COUNT(k) ((void)0)
+#endif
+
 // sincos(theta), then body(sin, cos, fast).  When every lane of the wave is in one of
 // sincos's region-B cases (x near pi/2; glibc_math.h sincos_b_*), the sincos is the
 // straight-line form of that case and body runs in the same basic block, so its own
@@ -512,28 +536,33 @@ GDEV void with_sincos(double theta, bool fast_ok, F&& body, bool div_ok = false)
     const bool tab = glibc::sincos_b_table_ok(theta), tay = glibc::sincos_b_taylor_ok(theta);
     if constexpr (FDIV) {
       if (__ballot(!(tab & div_ok)) == 0) {
+        PATH_COUNT(0);
         glibc::sincos_b_table(theta, &st, &ct);
         body(st, ct, true, std::true_type{});
         return;
       }
       if (__ballot(!(tay & div_ok)) == 0) {
+        PATH_COUNT(1);
         glibc::sincos_b_taylor(theta, &st, &ct);
         body(st, ct, true, std::true_type{});
         return;
       }
     }
     if (__ballot(!tab) == 0) {
+      PATH_COUNT(2);
       glibc::sincos_b_table(theta, &st, &ct);
       body(st, ct, true, std::false_type{});
       return;
     }
     if (__ballot(!tay) == 0) {
+      PATH_COUNT(2);
       glibc::sincos_b_taylor(theta, &st, &ct);
       body(st, ct, true, std::false_type{});
       return;
     }
   }
 #endif
+  PATH_COUNT(3);
   double st, ct;
   rsincos(theta, &st, &ct);
   body(st, ct, false, std::false_type{});
@@ -575,21 +604,6 @@ GDEV bool bl_div_ok(const DevScene& S, double r, double del, double l_z) {
   return S.div_fast && (fabs(r) < 0x1p100) & in_div_range(del) & (fabs(l_z) > 0x1p-200) & (fabs(l_z) < 0x1p100);
 }
 
-#ifndef GRT_KS_PATH_COUNT
-#define GRT_KS_PATH_COUNT 0  // diagnostic builds only: count rhs<KERR> evaluations per form
-#endif
-#if GRT_KS_PATH_COUNT
-// [0] wave-level fast-form evaluations, [1] IEEE-form, [2] / [3] the same in lanes
-__shared__ unsigned long long ks_path_lds[4];
-__device__ unsigned long long g_ks_path[4];
-GDEV void ks_path_count(int k) {
-  const uint64_t m = __ballot(1);  // the lanes evaluating this RHS together
-  if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) {
-    atomicAdd(&ks_path_lds[k], 1ull);
-    atomicAdd(&ks_path_lds[k + 2], (unsigned long long)__popcll(m));
-  }
-}
-#endif
 
 // ---- the ODE right-hand sides ----
 // MODE 0: the render's RHS.  MODE 1 / 2 (rhs_check_kernel only): region-B sincos (or no
@@ -747,16 +761,12 @@ GDEV void rhs(const DevScene& S, const RayConst& rc, const double* y, double* o)
     // The metric quotients without v_div_scale (div_fx) when every lane's state passes
     // ks_fd_ok (wave-uniform, like the region-B forms above)
     if (S.div_fast && __ballot(!ks_fd_ok(a, x, yy, z, S.ks_cap)) == 0) {
-#if GRT_KS_PATH_COUNT
-      ks_path_count(0);
-#endif
+      PATH_COUNT(0);
       body(std::true_type{});
       return;
     }
 #endif
-#if GRT_KS_PATH_COUNT
-    ks_path_count(1);
-#endif
+    PATH_COUNT(1);
     body(std::false_type{});
   } else {  // Euclidean, euclidean.rs:47-53
     o[0] = y[4];
@@ -1857,6 +1867,7 @@ GDEV void window_pass(const DevScene& S, const Workspace& ws, const RayConst& rc
                       const double* yn, double* c, bool& c_valid, uint64_t i, uint32_t& nrec, bool writer) {
   const uint64_t n = ws.n;
   if (!window_far<G, VOL>(S, y, yn)) {
+    PATH_COUNT(4);
     if (!c_valid) to_cart<G>(S, y, c);
     double cn[3];
     to_cart<G>(S, yn, cn);
@@ -1966,8 +1977,8 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
   // items present: the capacity, or the count the adaptive pass decided on the device
   const uint64_t n_items = wl.n_live ? (uint64_t)min((unsigned long long)wl.n_items, *wl.n_live) : wl.n_items;
   if (n_items == 0) return;  // an empty chunk of a supersample pass
-#if GRT_KS_PATH_COUNT
-  if (threadIdx.x < 4) ks_path_lds[threadIdx.x] = 0;  // ordered before use by the tables' barrier
+#if GRT_PATH_COUNT
+  if (threadIdx.x < 2 * NPATH) path_lds[threadIdx.x] = 0;  // ordered before use by the tables' barrier
 #endif
   glibc::tables_to_lds();  // whole block, before any lookup
   const int lane = threadIdx.x & 63;
@@ -2189,6 +2200,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
                    ? rkf_attempt<G, UNIT_H_COPY, false, NKL>(S, rc, y, h_cur, yn)
                    : rkf_attempt<G, false, false, NKL>(S, rc, y, h_cur, yn);
       n_att++;
+      PATH_COUNT(6);
 #if GRT_RAY_TIMES
       ray_att++;
 #endif
@@ -2223,6 +2235,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     }
 
     // ---------------- accepted step i (integrator.rs:100-162) --------------------
+    PATH_COUNT(5);
     h = h_next;
     i++;
     n_acc++;
@@ -2254,9 +2267,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
     atomicAdd(stats + 1, (unsigned long long)w_att);
     atomicAdd(stats + 2, (unsigned long long)w_rays);
   }
-#if GRT_KS_PATH_COUNT
+#if GRT_PATH_COUNT
   __syncthreads();  // every wave of the block has left its loop
-  if (threadIdx.x < 4) atomicAdd(&g_ks_path[threadIdx.x], ks_path_lds[threadIdx.x]);
+  if (threadIdx.x < 2 * NPATH) atomicAdd(&g_path[threadIdx.x], path_lds[threadIdx.x]);
 #endif
 }
 
@@ -2497,12 +2510,12 @@ hipError_t launch_rhs_check(int geometry, const DevScene* d_scene, const double*
   return hipGetLastError();
 }
 
-#if GRT_KS_PATH_COUNT
-hipError_t ks_path_read(unsigned long long* out, bool reset) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ks_path), sizeof(g_ks_path));
+#if GRT_PATH_COUNT
+hipError_t path_read(unsigned long long* out, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_path), sizeof(g_path));
   if (e == hipSuccess && reset) {
-    const unsigned long long z[4] = {0, 0, 0, 0};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_ks_path), z, sizeof(z));
+    const unsigned long long z[2 * NPATH] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_path), z, sizeof(z));
   }
   return e;
 }

@@ -51,8 +51,8 @@ hipError_t launch_arith_map(uint32_t samples, uint64_t seed, uint8_t* d_map, uin
                             hipStream_t stream);
 hipError_t launch_rhs_check(int geometry, const DevScene* d_scene, const double* d_states, const double* d_consts,
                             uint64_t n, double* d_out, uint8_t* d_pred, hipStream_t stream);
-#if GRT_KS_PATH_COUNT
-hipError_t ks_path_read(unsigned long long* out, bool reset);
+#if GRT_PATH_COUNT
+hipError_t path_read(unsigned long long* out, bool reset);  // 16 words
 #endif
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
 

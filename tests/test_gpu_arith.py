@@ -186,3 +186,38 @@ def test_rhs_kerr_bl_fast_form_matches_ieee(grt, gpu):
                    rng.uniform(-3, 3, n), np.zeros(n), np.zeros(n)], axis=1)
     consts = np.stack([rng.uniform(0.1, 10.0, n), lz, rng.uniform(-10.0, 100.0, n)], axis=1)
     print("kerr-bl", _check(grt, gpu, hs, st, consts))
+
+
+def _frame(grt, hs, rect, range_free):
+    fn = grt._lib.lib().grt_debug_range_free
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_int]
+    assert fn(1 if range_free else 0) == 0
+    try:
+        sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
+        r = sc.render_pixels(*rect, aux=True)
+    finally:
+        fn(1)
+    return r
+
+
+@pytest.mark.parametrize("case", ["c2", "c3", "c4"])
+def test_range_free_frames_equal_ieee_frames(grt, gpu, case):
+    """End to end: frames rendered with the range-free divisions / square roots and with
+    every one of them in the compiler's IEEE form (grt_debug_range_free(0):
+    DevScene::div_fast = 0) are identical bit for bit -- colours, classes, stop reasons,
+    step counts, hit counts.  C2 and C3 whole frames (configs[1], [2]); a 256^2 C4 crop
+    through the shadow edge and the disc at max-steps 1e5 (configs[3]'s scene)."""
+    if case == "c2":
+        hs, rect = host_scene(grt, "schwarzschild.toml", c2_opts(grt)), (0, 0, 1500, 1500)
+    elif case == "c3":
+        hs, rect = host_scene(grt, "kerr-bl.toml", c3_opts(grt)), (0, 0, 1500, 1500)
+    else:
+        hs, rect = host_scene(grt, "kerr.toml", c4_opts(grt, max_steps=100000)), (1920, 1920, 256, 256)
+    a = _frame(grt, hs, rect, True)
+    b = _frame(grt, hs, rect, False)
+    assert np.array_equal(a.xyza64.view(np.uint64), b.xyza64.view(np.uint64))
+    for k in ("ray_class", "status", "stop_reason", "steps", "hits"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    print(case, "rays", a.stats["rays"], "steps", a.stats["accepted_steps"], "ms range-free / IEEE",
+          round(a.stats["kernel_ms"], 1), round(b.stats["kernel_ms"], 1))
