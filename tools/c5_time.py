@@ -9,6 +9,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import gr_raytracer_amd as g  # noqa: E402
+import os  # noqa: E402
+if "GRT_BLOCKS_PER_CU" in os.environ:  # integrate-kernel blocks per CU (default: 2 x waves per SIMD)
+    g._lib.check(g._lib.lib().grt_set_launch_config(int(os.environ["GRT_BLOCKS_PER_CU"]), 256), "grt_set_launch_config")
 
 opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, max_steps=100000)
 hs = g.HostScene(str(ROOT / "tests/golden/scenes/schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
