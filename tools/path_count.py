@@ -3,7 +3,7 @@
 times a wave executed it (counted by its first active lane) and how many lanes did.
 Kerr-Schild RHS: 0 range-free, 1 IEEE.  Schwarzschild / KerrBL RHS: 0 region-B table
 with range-free divisions, 1 region-B Taylor with them, 2 region B with IEEE divisions,
-3 general sincos.  All: 4 near-field window pass, 5 accepted step, 6 attempt.
+3 general sincos (7: of those, with the range-free divisions).  All: 4 near-field window pass, 5 accepted step, 6 attempt.
 usage: tools/path_count.py c2|c3|c4 (c4: row-band shard 2 of 8)"""
 import ctypes as C
 import hashlib
@@ -43,6 +43,9 @@ names = (["rhs_range_free", "rhs_ieee"] if which == "c4" else
 names += ["near_window", "accepted_general_path", "attempt"]
 keys = [0, 1] if which == "c4" else [0, 1, 2, 3]
 keys += [4, 5, 6]
+if which != "c4":  # general sincos with the range-free divisions (GRT_FAST_DIV_GEN builds)
+    names.append("rhs_general_range_free")
+    keys.append(7)
 out = {"workload": which, "kernel_ms": r.stats["kernel_ms"], "wall_s": round(time.time() - t, 3),
        "accepted_steps": r.stats["accepted_steps"], "attempts_total": r.stats["attempts"],
        "md5": hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12]}
