@@ -794,15 +794,16 @@ GDEV double quad_bcast(double v) {
 // sub + 1 (lane 3 repeats component 3), and the three components are broadcast across
 // the quad.  Every value comes out of the same operations as in rhs<KERR>, so o is
 // bit-identical in all four lanes; the quad's lanes must be active together.
-GDEV void rhs_ks_quad(const DevScene& S, const double* y, double* o, int sub) {
+template <bool FD>
+GDEV void rhs_ks_quad_form(const DevScene& S, const double* y, double* o, int sub) {
   const double radius = S.radius, a = S.a;
   const double x = y[1], yy = y[2], z = y[3];
   const double p[4] = {y[4], y[5], y[6], y[7]};
   double Gc[4][4];
-  ks_metric_contra(radius, a, x, yy, z, Gc);
+  ks_metric_contra<FD>(radius, a, x, yy, z, Gc);
   double xdot[4];
   mat_vec(Gc, p, xdot);
-  const double acc = ks_accel(radius, a, sub < 3 ? sub + 1 : 3, x, yy, z, Gc, p);
+  const double acc = ks_accel<FD>(radius, a, sub < 3 ? sub + 1 : 3, x, yy, z, Gc, p);
   o[0] = xdot[0];
   o[1] = xdot[1];
   o[2] = xdot[2];
@@ -811,6 +812,17 @@ GDEV void rhs_ks_quad(const DevScene& S, const double* y, double* o, int sub) {
   o[5] = quad_bcast<0>(acc);
   o[6] = quad_bcast<1>(acc);
   o[7] = quad_bcast<2>(acc);
+}
+// with rhs<KERR>'s range-free metric quotients and square roots when every lane's state
+// passes ks_fd_ok (the quad's four lanes hold the same state)
+GDEV void rhs_ks_quad(const DevScene& S, const double* y, double* o, int sub) {
+#if GRT_FAST_DIV_KS
+  if (S.div_fast && __ballot(!ks_fd_ok(S.a, y[1], y[2], y[3], S.ks_cap)) == 0) {
+    rhs_ks_quad_form<true>(S, y, o, sub);
+    return;
+  }
+#endif
+  rhs_ks_quad_form<false>(S, y, o, sub);
 }
 
 template <int G, bool QUAD>
