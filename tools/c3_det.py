@@ -11,6 +11,9 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import gr_raytracer_amd as g  # noqa: E402
+import os  # noqa: E402
+if "GRT_BLOCKS_PER_CU" in os.environ:  # integrate-kernel blocks per CU (default: 2 x waves per SIMD)
+    g._lib.check(g._lib.lib().grt_set_launch_config(int(os.environ["GRT_BLOCKS_PER_CU"]), 256), "grt_set_launch_config")
 
 out = sys.argv[1]
 runs = int(sys.argv[2]) if len(sys.argv) > 2 else 3
