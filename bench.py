@@ -4,7 +4,10 @@ Default workload (BASELINE.json configs[1]): 1500x1500 scene-definitions/schwarz
 --max-steps=1e5, camera from README.md:63 (--camera-position=-16,0,3.5 --theta=-3.142),
 1 sample per pixel (adaptive sampling off).  One bench "step" = one full 1500x1500
 frame traced on the GPU (every pixel integrated to its stop condition, every window
-tested against the Sphere and the Disc, every pixel shaded).
+tested against the Sphere and the Disc, every pixel shaded).  Two frames are in flight
+(--inflight): frame k runs on slot k mod 2, each slot with its own Scene workspace, output
+buffers and stream, so that one frame's end of pass overlaps the next frame's start; every
+frame is traced in full, and the timed region ends when the last one is done.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak
 scaling over a batch of frames: rank r renders frame r of a camera fly-by (the camera
@@ -247,46 +250,66 @@ def run_c2(args, rank, world, local_rank, dev):
     lib = L.lib()
     opts = c2_opts(g, frame=rank)
     hs = g.HostScene(str(SCENES / "schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
-    scene = g.Scene(hs.desc_ptr(), keepalive=hs)
     rows, cols = opts.height, opts.width
     n = rows * cols
-    xyza = torch.empty((n, 4), dtype=torch.float32, device=dev)
-    cls = torch.empty(n, dtype=torch.uint8, device=dev)
-    status = torch.empty(n, dtype=torch.uint8, device=dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    gather = [torch.empty_like(xyza) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # Frames in flight: frame k goes to slot k mod F, each slot with its own Scene (device
+    # workspace, counters), output buffers and stream, so that the persistent kernel's end of
+    # pass (the last ray lifetime at falling lane occupancy) overlaps the next frame's start.
+    F = max(1, args.inflight)
+    gathered = world > 1 or args.self_gather  # --self-gather: the gather path in a group of one
+    slots = []
+    for _ in range(F):
+        slots.append({
+            "scene": g.Scene(hs.desc_ptr(), keepalive=hs),
+            "xyza": torch.empty((n, 4), dtype=torch.float32, device=dev),
+            "cls": torch.empty(n, dtype=torch.uint8, device=dev),
+            "status": torch.empty(n, dtype=torch.uint8, device=dev),
+            "stats": torch.zeros(4, dtype=torch.int64, device=dev),
+            "stream": torch.cuda.current_stream(dev) if F == 1 else torch.cuda.Stream(dev),
+            "gather": [torch.empty((n, 4), dtype=torch.float32, device=dev) for _ in range(world)]
+            if (gathered and rank == 0) else None,
+        })
 
-    def one_step():
-        L.check(lib.grt_render_pixels_async(scene._s, local_rank, stream.cuda_stream, 0, 0, rows, cols,
-                                            xyza.data_ptr(), cls.data_ptr(), status.data_ptr(), None, None, None,
-                                            stats.data_ptr()), "grt_render_pixels_async")
+    def one_step(k, ev=None):
+        s = slots[k % F]
+        st = s["stream"]
+        if ev is not None:
+            ev[0].record(st)
+        L.check(lib.grt_render_pixels_async(s["scene"]._s, local_rank, st.cuda_stream, 0, 0, rows, cols,
+                                            s["xyza"].data_ptr(), s["cls"].data_ptr(), s["status"].data_ptr(),
+                                            None, None, None, s["stats"].data_ptr()), "grt_render_pixels_async")
+        if ev is not None:
+            ev[1].record(st)
+        if gathered:  # on the slot's stream: the gather waits for this frame only, and the
+            with torch.cuda.stream(st):  # slot's next frame waits for the gather
+                dist.gather(s["xyza"], gather_list=s["gather"], dst=0, async_op=True).wait()
 
-    for _ in range(args.warmup):
-        one_step()
-        if world > 1:
-            dist.gather(xyza, gather_list=gather, dst=0)
+    for _ in range(args.warmup):  # a warm-up step renders one frame in every slot
+        for j in range(F):
+            one_step(j)
     torch.cuda.synchronize(dev)
 
-    stats.zero_()
+    for s in slots:
+        s["stats"].zero_()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
-        one_step()
-        ev[k][1].record(stream)
-        if world > 1:
-            dist.gather(xyza, gather_list=gather, dst=0)
+        one_step(k, ev[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    counters = stats.cpu().tolist()  # accepted, attempts, rays, overflows (summed over K frames)
-    accepted, attempts = counters[0], counters[1]
+    # the device time per frame: first frame's start to last frame's end over K (with one
+    # frame in flight, the mean launch duration)
+    if F == 1:
+        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    else:
+        kernel_ms = ev[0][0].elapsed_time(ev[-1][1]) / args.steps
+    counters = [sum(v) for v in zip(*(s["stats"].cpu().tolist() for s in slots))]
+    accepted, attempts = counters[0], counters[1]  # summed over K frames
 
     elapsed, total_acc, total_att = reduce_over_ranks(elapsed, accepted, attempts, world, dev)
     if rank != 0:
@@ -302,6 +325,7 @@ def run_c2(args, rank, world, local_rank, dev):
         "config": {"workload": "C2: 1500x1500 schwarzschild.toml, max-steps=1e5, camera -16,0,3.5 "
                                "theta=-3.142, 1 spp (adaptive off); one step = one frame per GPU",
                    "frame_pixels": n, "parallelism": f"frames x{world} (one frame per GPU), RCCL gather",
+                   "frames_in_flight": F,
                    "steps_per_gpu_per_s": total_acc / elapsed / world,
                    "attempts_per_accepted": total_att / max(total_acc, 1.0),
                    "frame_wall_s_per_gpu": elapsed / args.steps},
@@ -310,6 +334,11 @@ def run_c2(args, rank, world, local_rank, dev):
                              "<0.01%)"),
         "cpu_baseline": None,
     }
+    line["roofline"]["kernel_ms_basis"] = (
+        "mean launch duration (HIP events on the launch stream)" if F == 1 else
+        f"device time per frame with {F} frames in flight: first frame's start event to last frame's end event "
+        f"/ K (HIP events on the slots' streams); a single launch's duration overlaps its neighbours' "
+        f"(rocprof: the spacing of consecutive integrate-kernel ends, tools/kernel_period.py)")
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(g, "c2")
     return line
@@ -457,7 +486,11 @@ def main() -> None:
     ap.add_argument("--size", type=int, default=4096, help="c4: frame edge (4096 = configs[3])")
     ap.add_argument("--band-rows", type=int, default=16, help="c4: rows per cyclic band")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="c2: frames in flight (one stream and workspace each); 1 = one frame after another")
     ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--self-gather", action="store_true", help="c2, one GPU: run the multi-GPU gather path "
+                    "in a process group of one (a check of the streams and RCCL gathers)")
     args = ap.parse_args()
 
     import torch
@@ -470,7 +503,7 @@ def main() -> None:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    elif args.workload == "c4":  # the c4 loop uses barriers: a group of one
+    elif args.workload == "c4" or args.self_gather:  # barriers / the gather path: a group of one
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(f"cuda:{local_rank}"))

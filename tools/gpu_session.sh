@@ -9,7 +9,9 @@
 #   suite=EXPR             pytest -m gpu -k EXPR
 #   smoke                  __graft_entry__.smoke()
 #   bench                  bench.py (C2 headline line)
-#   benchprof              rocprofv3 --kernel-trace --stats of bench.py --steps 5
+#   benchprof              rocprofv3 --kernel-trace --stats of bench.py --steps 5, + tools/kernel_period.py
+#   bench_seq              bench.py --inflight 1 (one frame after another)
+#   bench_gather           bench.py --self-gather (the multi-GPU gather path in a group of one)
 #   bench_c4               bench.py --workload c4 (the whole C4 frame) under rocprofv3 --stats
 #   pmc=c2|c3|c4|c4full    PMC passes (tools/run_pmc.sh; c4full: FETCH / WRITE only)
 #   shards                 the eight C4 1/8 row-band shards (tools/c4_shard_time.py)
@@ -46,7 +48,17 @@ for step in "$@"; do
     benchprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
         python3 bench.py --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err \
-        || { tail -20 $OUT/bench_prof.err >&2; exit 1; } ;;
+        || { tail -20 $OUT/bench_prof.err >&2; exit 1; }
+      python3 tools/kernel_period.py $OUT/prof/run_kernel_trace.csv "integrate_kernel<1, false>" 5 \
+        > $OUT/kernel_period.json && cut -c1-600 $OUT/kernel_period.json >&2 ;;
+    bench_seq)
+      timeout -k 10 600 python3 bench.py --inflight 1 > $OUT/bench_seq.json 2> $OUT/bench_seq.err \
+        || { tail -20 $OUT/bench_seq.err >&2; exit 1; }
+      cut -c1-400 $OUT/bench_seq.json >&2 ;;
+    bench_gather)
+      MASTER_PORT=29533 timeout -k 10 600 python3 bench.py --self-gather --no-cpu-baseline \
+        > $OUT/bench_gather.json 2> $OUT/bench_gather.err || { tail -20 $OUT/bench_gather.err >&2; exit 1; }
+      cut -c1-400 $OUT/bench_gather.json >&2 ;;
     bench_c4)
       timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- \
         python3 bench.py --workload c4 --steps 1 --warmup 0 > $OUT/bench_c4.json 2> $OUT/bench_c4.err \
