@@ -1,7 +1,10 @@
 """C2 frames back to back on one stream against frames alternating over two streams, each
 stream with its own Scene (workspace, counters), so that one frame's end of pass can
 overlap the next frame's start.  Prints one JSON line per run (wall ms per frame, md5 of
-each frame's outputs).  Usage: pipeline_probe.py [K] [ROUNDS]"""
+each frame's outputs).  Usage: pipeline_probe.py [K] [ROUNDS]
+Env: SLOTS (frames in flight in the "pipe" mode, default 2), LAUNCH=blocks_per_cu,threads
+(grt_set_launch_config), MODES (default "seq,pipe")."""
+import os
 import hashlib
 import json
 import sys
@@ -20,14 +23,19 @@ K = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 dev = torch.device("cuda:0")
 lib = L.lib()
+if os.environ.get("LAUNCH"):
+    bpc, thr = (int(v) for v in os.environ["LAUNCH"].split(","))
+    L.check(lib.grt_set_launch_config(bpc, thr), "grt_set_launch_config")
+F = int(os.environ.get("SLOTS", "2"))
+MODES = os.environ.get("MODES", "seq,pipe").split(",")
 opts = bench.c2_opts(g)
 hs = g.HostScene(str(ROOT / "tests/golden/scenes/schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
-scenes = [g.Scene(hs.desc_ptr(), keepalive=hs) for _ in range(2)]
+scenes = [g.Scene(hs.desc_ptr(), keepalive=hs) for _ in range(F)]
 n = opts.height * opts.width
 outs = [(torch.empty((n, 4), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.uint8, device=dev),
          torch.empty(n, dtype=torch.uint8, device=dev), torch.zeros(4, dtype=torch.int64, device=dev))
-        for _ in range(2)]
-streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        for _ in range(F)]
+streams = [torch.cuda.Stream(dev) for _ in range(F)]
 
 
 def frame(j, stream):
@@ -51,17 +59,18 @@ def run(mode):
         if mode == "seq":
             frame(0, streams[0])
         else:
-            frame(k % 2, streams[k % 2])
+            frame(k % F, streams[k % F])
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     acc = sum(int(o[3][0]) for o in outs)
-    return {"mode": mode, "frames": K, "ms_per_frame": dt / K * 1e3, "steps_per_s": acc / dt,
-            "md5": [md5(0)] + ([md5(1)] if mode == "pipe" else [])}
+    return {"mode": mode, "slots": F if mode == "pipe" else 1, "launch": os.environ.get("LAUNCH", ""), "frames": K,
+            "ms_per_frame": dt / K * 1e3, "steps_per_s": acc / dt,
+            "md5": [md5(j) for j in range(F if mode == "pipe" else 1)]}
 
 
-frame(0, streams[0])
-frame(1, streams[1])
-torch.cuda.synchronize(dev)
+for j in range(F):
+    frame(j, streams[j])
+    torch.cuda.synchronize(dev)
 for _ in range(ROUNDS):
-    for mode in ("seq", "pipe"):
+    for mode in MODES:
         print(json.dumps(run(mode)), flush=True)
