@@ -328,6 +328,7 @@ def run_c2(args, rank, world, local_rank, dev):
                    "frames_in_flight": F,
                    "steps_per_gpu_per_s": total_acc / elapsed / world,
                    "attempts_per_accepted": total_att / max(total_acc, 1.0),
+                   "accepted_steps_per_frame": total_acc / (args.steps * world),
                    "frame_wall_s_per_gpu": elapsed / args.steps},
         "roofline": roofline("c2", "schwarzschild", accepted / args.steps, attempts / args.steps, kernel_ms, n,
                              "grt::integrate_kernel<1, false> (Schwarzschild; events also span shade_kernel<1, 0>, "
