@@ -27,6 +27,7 @@ namespace {
 int g_blocks_per_cu = 0;
 int g_range_free = 1;  // grt_debug_range_free: 0 = every division and sqrt in its IEEE form (tests)
 int g_threads = 256;
+int g_probe_quad = -1;  // Kerr-Schild probe on quads: -1 auto, 0 never, 1 always (grt_debug_probe_keys)
 int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
 int g_two_ended = 1;  // grt_set_two_ended: probe-ordered traces take the queue from both ends
 long long g_tail = -1;  // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
@@ -535,7 +536,11 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   uint32_t* ord = (uint32_t*)take(n * 4);
   void* temp = take(temp_bytes);
   const uint32_t cap = probe_cap(s);
-  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, cap, probe, stream));
+  // Kerr-Schild probe rays on quads when they fill at most 2 waves per SIMD that way
+  // (probe_quad_kernel: a C4 1/8 shard's 32,768 probes); above that the one-lane probe,
+  // whose pass is then bound by its work, not by one probe's latency
+  const bool quad = g_probe_quad > 0 || (g_probe_quad < 0 && n <= (uint64_t)dc.cus * 128);
+  HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, cap, probe, quad, stream));
   HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, cap, keys, keys_sorted, idx, ord, temp, &temp_bytes, stream));
   *order = ord;
   return 0;
@@ -800,6 +805,33 @@ int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n,
   return 0;
 }
 #endif
+
+// Test hook (not in grt_api.h): the probe keys (probe_kernel / probe_quad_kernel) of a
+// row-band shard with the probe forced onto quads (quad = 1) or onto one lane per ray (0).
+int grt_debug_probe_keys(grt_scene* s, int device, const grt_row_shard* sh, int quad, uint32_t* keys_out,
+                         uint64_t n_tiles) {
+  if (!s || !sh || !keys_out || (quad != 0 && quad != 1)) return fail(-EINVAL, "probe keys: bad argument");
+  DeviceCopy* dc;
+  int rc;
+  if ((rc = ensure_device(s, device, &dc))) return rc;
+  std::lock_guard<std::mutex> lk(dc->mu);
+  HIP_TRY(hipSetDevice(device));
+  grt::WorkList wl = rect_worklist(0, 0, grt_shard_row_count((uint32_t)s->desc.camera.rows, sh),
+                                   (uint32_t)s->desc.camera.cols);
+  wl.band_rows = sh->band_rows;
+  wl.shard = sh->shard;
+  wl.n_shards = sh->n_shards;
+  if (wl.n_items / 64 != n_tiles || wl.n_items % 64 != 0) return fail(-EINVAL, "tile count differs");
+  const uint32_t* order = nullptr;
+  const int saved = g_probe_quad;
+  g_probe_quad = quad;
+  rc = enqueue_tile_order(s, *dc, wl, nullptr, &order);
+  g_probe_quad = saved;
+  if (rc) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(keys_out, dc->sched_mem, n_tiles * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 // Test hook (not in grt_api.h): the range-free divisions and square root (geodesic.hip
 // div_inrange, div2_inrange, div_fx, sqrt_fx) against the compiler's over the exponent

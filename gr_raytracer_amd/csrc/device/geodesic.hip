@@ -2767,9 +2767,64 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
   steps_out[t] = key;
 }
 
+// probe_kernel<KERR> with each probe ray on the 4 lanes of a quad (rhs_ks_quad, as in
+// tail_kernel): the same operations on the same values, so the same keys (GPU test
+// tests/test_gpu_schedule.py).  For a pass of few probe rays (a 1/8 row-band shard of
+// C4: 32,768 tiles, 0.5 waves per SIMD as one lane each) the pass lasts as long as its
+// capped probes take to run `cap` steps at one wave's latency; splitting each RHS over a
+// quad cuts that latency, at 4x the lanes (2 waves per SIMD here).
+__global__ void __launch_bounds__(256, 2) probe_quad_kernel(const DevScene* __restrict__ Sp, WorkList wl,
+                                                            uint32_t n_tiles, uint32_t cap,
+                                                            uint32_t* __restrict__ steps_out) {
+  constexpr int G = GRT_GEOM_KERR;
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;  // the quad's tile
+  const int sub = threadIdx.x & 3;
+  if (t >= n_tiles) return;  // the whole quad
+  const uint32_t tr = t / wl.tiles_x, tc = t % wl.tiles_x;
+  const uint32_t r = min(tr * 8 + 3, wl.rows - 1), c = min(tc * 8 + 3, wl.cols - 1);
+  double y[8];
+  RayConst rc;
+  init_ray<G>(S, (double)(wl.row0 + shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, r)),
+              (double)(wl.col0 + c), y, rc);
+  const uint64_t end = S.max_steps < (uint64_t)cap ? S.max_steps : (uint64_t)cap;
+  uint64_t i = 1;
+  double h = S.step_size;
+  for (; i < end; ++i) {  // identical decisions in the quad's four lanes
+    double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
+    int retries = 0, ctl;
+    do {
+      const double err_sq = rkf_attempt<G, false, true>(S, rc, y, h_cur, yn, sub);
+      ctl = step_control(S, err_sq, h_cur, retries, h_next);
+    } while (ctl == STEP_RETRY);
+    if (ctl == STEP_FAILED) break;
+    h = h_next;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = yn[k];
+    double cc[3];
+    bool c_valid = false;
+    if (should_stop<G>(S, y, cc, c_valid, i) != GRT_STOP_NONE) break;
+  }
+  uint32_t key = (uint32_t)i;
+  if (i >= end) {
+    key = cap;
+    if (S.has_horizon && S.horizon_r > 0.0) {
+      const double d = (sqrt(ks_r_sqr(S.a, y[1], y[2], y[3])) - S.horizon_r) / S.horizon_r * 1073741824.0;
+      if (d > 0.0) key = cap + (uint32_t)fmin(d, (double)(0xffffffffu - cap));  // NaN: stays cap
+    }
+  }
+  if (sub == 0) steps_out[t] = key;
+}
+
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,
-                        uint32_t* d_steps, hipStream_t stream) {
+                        uint32_t* d_steps, bool quad, hipStream_t stream) {
   if (n_tiles == 0) return hipSuccess;
+  if (quad && geometry == GRT_GEOM_KERR) {
+    hipLaunchKernelGGL(probe_quad_kernel, dim3((n_tiles * 4ull + 255) / 256), dim3(256), 0, stream, d_scene, wl,
+                       n_tiles, cap, d_steps);
+    return hipGetLastError();
+  }
   const unsigned blocks = (n_tiles + 63) / 64;
   switch (geometry) {
     case GRT_GEOM_EUCLIDEAN:

@@ -23,8 +23,9 @@ hipError_t set_ray_times(unsigned long long* p);
 constexpr int TAIL_RAYS_PER_BLOCK = 256 / 4;
 
 // Work-order probe: steps of one ray per 8x8 tile of `wl` (rectangle mode), capped.
+// quad (Kerr-Schild only): each probe ray on a quad of lanes (probe_quad_kernel), same keys.
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,
-                        uint32_t* d_steps, hipStream_t stream);
+                        uint32_t* d_steps, bool quad, hipStream_t stream);
 // Tile queue order from the probe keys (schedule.hip): 3x3-dilated keys (edge tiles of a
 // region of probes that reached `cap` boosted), sorted descending (stable).  `temp` /
 // `temp_bytes`: scratch, query with temp == NULL.
