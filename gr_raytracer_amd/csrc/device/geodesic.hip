@@ -857,10 +857,10 @@ struct Dim {
 // that RHS evaluation.  Values are stored and re-read unchanged: the arithmetic is the same.
 constexpr int KL_STRIDE = 256;
 __shared__ double kl_buf[GRT_KL_STAGES * 8 * KL_STRIDE];  // 16 KB per stage, only in kernels that use it
-GDEV void kl_put(int j, const double* k, int D) {
+GDEV void kl_put(int j, const double* k, int D, int skip = -1) {
 #pragma unroll
   for (int i = 0; i < 8; ++i)
-    if (i < D) kl_buf[(j * 8 + i) * KL_STRIDE + (int)threadIdx.x] = k[i];
+    if (i < D && i != skip) kl_buf[(j * 8 + i) * KL_STRIDE + (int)threadIdx.x] = k[i];
 }
 // threadIdx.x, opaque to the compiler and ordered after `dep`
 GDEV int kl_slot_after(double dep) {
@@ -879,15 +879,33 @@ GDEV constexpr bool rhs_reads(int i) {
   return i == 1 || i == 2 || i >= 4;  // Schwarzschild, EuclideanSpherical, KerrBL: r, theta, velocities
 }
 
+// The state component whose derivative the RHS sets to the constant 0.0, or -1: p_t in
+// Kerr-Schild (kerr.rs:233-241, the metric does not depend on t).  Its stage values are
+// k_j = h * 0.0 = kz for every stage j of an attempt (kz = +0 for h > 0), so each of
+// rkf45_step's left-to-right sums for it, y + c_1 kz + ... + c_m kz, is a sum of signed
+// zeros (or NaNs) onto y, and IEEE addition gives it in one step: y + kz when every
+// coefficient is >= 0 (each term carries kz's sign), y + kz * kz when the signs are mixed
+// (some term is +0, which makes any later zero sum +0; kz * kz is +0, or NaN for a NaN
+// kz).  Its error term (a mixed sum, no y) squares to +0: kz * kz as well.  Same bits as
+// the full sums for every y, signed zeros and NaN included.
+template <int G>
+GDEV constexpr int zero_k() {
+  return G == GRT_GEOM_KERR ? 4 : -1;
+}
+
 // nalgebra norm(): 8-accumulator unrolled dot, ((a0+a4) + (a1+a5)) + (a2+a6) + (a3+a7)
+// z >= 0: e[z] * e[z] is given as zz (zero_k)
 template <int D>
-GDEV double err_norm_sq(const double* e) {
+GDEV double err_norm_sq(const double* e, int z = -1, double zz = 0.0) {
   double res;
   if constexpr (D == 8) {
-    res = e[0] * e[0] + e[4] * e[4];
-    res += e[1] * e[1] + e[5] * e[5];
-    res += e[2] * e[2] + e[6] * e[6];
-    res += e[3] * e[3] + e[7] * e[7];
+    double sq[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sq[i] = (i == z) ? zz : e[i] * e[i];
+    res = sq[0] + sq[4];
+    res += sq[1] + sq[5];
+    res += sq[2] + sq[6];
+    res += sq[3] + sq[7];
   } else {
     res = e[0] * e[0] + e[4] * e[4];
     res += e[1] * e[1] + e[5] * e[5];
@@ -1007,45 +1025,52 @@ GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, 
     return rkf_attempt_fold<G, UNIT_H, QUAD, NKL>(S, rc, y, h, yn, sub);
   }
   constexpr int D = Dim<G>::D;
+  constexpr int Z = zero_k<G>();  // component with k_j = kz in every stage (zero_k)
   double k1[8], k2[8], k3[8], k4[8], k5[8], k6[8], tmp[8], o[8];
   int t = 0;  // LDS slot, re-derived after each stage (kl_slot_after)
   // stage j's value k_j[i] (from LDS when parked there)
 #define KV(j, i) (((j) <= NKL) ? kl_get(t, (j) - 1, (i)) : k##j[i])
   rhs_sel<G, QUAD>(S, rc, y, o, sub);
+  // signs: B21 > 0; B31, B32 > 0; B4x, B5x, B6x mixed; CH1..CH6 >= 0; CT mixed
+  const double kz = Z < 0 ? 0.0 : (UNIT_H ? o[Z < 0 ? 0 : Z] : h * o[Z < 0 ? 0 : Z]);
+  const double kzz = kz * kz;
 #pragma unroll
   for (int i = 0; i < D; ++i) k1[i] = UNIT_H ? o[i] : h * o[i];
-  if (NKL >= 1) kl_put(0, k1, D);
+  if (NKL >= 1) kl_put(0, k1, D, Z);
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B21 * k1[i];
+  for (int i = 0; i < D; ++i) tmp[i] = (i == Z) ? y[i] + kz : y[i] + B21 * k1[i];
   if (D < 8) { tmp[6] = 0.0; tmp[7] = 0.0; }
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k2[i] = UNIT_H ? o[i] : h * o[i];
-  if (NKL >= 2) kl_put(1, k2, D);
+  if (NKL >= 2) kl_put(1, k2, D, Z);
   if (NKL >= 1) t = kl_slot_after(k2[D - 1]);
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B31 * KV(1, i) + B32 * k2[i];
+  for (int i = 0; i < D; ++i) tmp[i] = (i == Z) ? y[i] + kz : y[i] + B31 * KV(1, i) + B32 * k2[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k3[i] = UNIT_H ? o[i] : h * o[i];
-  if (NKL >= 3) kl_put(2, k3, D);
+  if (NKL >= 3) kl_put(2, k3, D, Z);
   if (NKL >= 1) t = kl_slot_after(k3[D - 1]);
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B41 * KV(1, i) + B42 * KV(2, i) + B43 * k3[i];
+  for (int i = 0; i < D; ++i)
+    tmp[i] = (i == Z) ? y[i] + kzz : y[i] + B41 * KV(1, i) + B42 * KV(2, i) + B43 * k3[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k4[i] = UNIT_H ? o[i] : h * o[i];
-  if (NKL >= 4) kl_put(3, k4, D);
+  if (NKL >= 4) kl_put(3, k4, D, Z);
   if (NKL >= 1) t = kl_slot_after(k4[D - 1]);
 #pragma unroll
-  for (int i = 0; i < D; ++i) tmp[i] = y[i] + B51 * KV(1, i) + B52 * KV(2, i) + B53 * KV(3, i) + B54 * k4[i];
+  for (int i = 0; i < D; ++i)
+    tmp[i] = (i == Z) ? y[i] + kzz : y[i] + B51 * KV(1, i) + B52 * KV(2, i) + B53 * KV(3, i) + B54 * k4[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k5[i] = UNIT_H ? o[i] : h * o[i];
   if (NKL >= 1) t = kl_slot_after(k5[D - 1]);
 #pragma unroll
   for (int i = 0; i < D; ++i)
-    tmp[i] = y[i] + B61 * KV(1, i) + B62 * KV(2, i) + B63 * KV(3, i) + B64 * KV(4, i) + B65 * k5[i];
+    tmp[i] = (i == Z) ? y[i] + kzz
+                      : y[i] + B61 * KV(1, i) + B62 * KV(2, i) + B63 * KV(3, i) + B64 * KV(4, i) + B65 * k5[i];
   rhs_sel<G, QUAD>(S, rc, tmp, o, sub);
 #pragma unroll
   for (int i = 0; i < D; ++i) k6[i] = UNIT_H ? o[i] : h * o[i];
@@ -1053,6 +1078,11 @@ GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, 
   double e[8];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
+    if (i == Z) {  // e[Z] only enters the norm as e[Z]^2 = kz * kz
+      yn[i] = y[i] + kz;
+      e[i] = 0.0;
+      continue;
+    }
     const double a1 = KV(1, i), a2 = KV(2, i), a3 = KV(3, i), a4 = KV(4, i);
     yn[i] = y[i] + CH1 * a1 + CH2 * a2 + CH3 * a3 + CH4 * a4 + CH5 * k5[i] + CH6 * k6[i];
     e[i] = CT1 * a1 + CT2 * a2 + CT3 * a3 + CT4 * a4 + CT5 * k5[i] + CT6 * k6[i];
@@ -1062,7 +1092,7 @@ GDEV double rkf_attempt(const DevScene& S, const RayConst& rc, const double* y, 
     yn[6] = 0.0;
     yn[7] = 0.0;
   }
-  return err_norm_sq<D>(e);
+  return err_norm_sq<D>(e, Z, kzz);
 }
 
 // ---- chart helpers ----
