@@ -484,8 +484,11 @@ grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_
 // H_MAX = 1 (C4: 15825-15900 steps for max_radius 15000), so 1.3 x max_radius still
 // tells them from the long rays while the capped probes (which run the whole cap) end
 // sooner: C4's probe pass 1.86 s -> ~1.2 s per 1/8 shard.  Scheduling only.
+#ifndef GRT_PROBE_CAP_SCALE
+#define GRT_PROBE_CAP_SCALE 1.3
+#endif
 static uint32_t probe_cap(const grt_scene* s) {
-  const double c = 1.3 * s->desc.max_radius;
+  const double c = GRT_PROBE_CAP_SCALE * s->desc.max_radius;
   return c >= (double)PROBE_CAP ? PROBE_CAP : (c <= 4096.0 ? 4096u : (uint32_t)c);
 }
 

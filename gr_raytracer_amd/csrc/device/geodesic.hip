@@ -2753,6 +2753,25 @@ hipError_t launch_health(int geometry, const DevScene* d_scene, const WorkList& 
 // distance they have left predicts the ray's length (log-log correlation 0.98 with the
 // probe pixel's own count; the 300 tiles with a ray past 8e5 steps are among the 311
 // largest keys but 11; tools/c4_probe_features.py), so the longest tiles are queued first.
+#ifndef GRT_PROBE_ESCAPE
+#define GRT_PROBE_ESCAPE 0  // experiment: end an outward-bound probe beyond 10 radii early
+#endif
+// Experiment (GRT_PROBE_ESCAPE, Kerr-Schild): a probe moving outward beyond 10 horizon
+// scales escapes; its key becomes cap - 1 (below every capped probe's, as its ray is
+// shorter than theirs), so a cap below the escaping rays' length still ranks them.
+template <int G>
+GDEV bool probe_escaped(const DevScene& S, const double* y, double& r_prev, uint32_t cap, uint32_t* key) {
+  if constexpr (G != GRT_GEOM_KERR || !GRT_PROBE_ESCAPE) {
+    return false;
+  } else {
+    const double r = sqrt(ks_r_sqr(S.a, y[1], y[2], y[3]));
+    const bool out = r > 10.0 * S.radius && r > r_prev;
+    r_prev = r;
+    if (out) *key = cap - 1;
+    return out;
+  }
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ Sp, WorkList wl, uint32_t n_tiles,
                                                    uint32_t cap, uint32_t* __restrict__ steps_out) {
@@ -2769,6 +2788,9 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
   const uint64_t end = S.max_steps < (uint64_t)cap ? S.max_steps : (uint64_t)cap;
   uint64_t i = 1;
   double h = S.step_size;
+  double r_prev = 0.0;
+  uint32_t key = 0;
+  bool escaped = false;
   for (; i < end; ++i) {
     double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
     int retries = 0, ctl;
@@ -2783,9 +2805,10 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
     double cc[3];
     bool c_valid = false;
     if (should_stop<G>(S, y, cc, c_valid, i) != GRT_STOP_NONE) break;
+    if ((escaped = probe_escaped<G>(S, y, r_prev, cap, &key))) break;
   }
-  uint32_t key = (uint32_t)i;
-  if (i >= end) {
+  if (!escaped) key = (uint32_t)i;
+  if (!escaped && i >= end) {
     key = cap;
     const bool horizon = G == GRT_GEOM_SCHWARZSCHILD || ((G == GRT_GEOM_KERR || G == GRT_GEOM_KERR_BL) && S.has_horizon);
     if (horizon && S.horizon_r > 0.0) {
@@ -2821,6 +2844,9 @@ __global__ void __launch_bounds__(256, 2) probe_quad_kernel(const DevScene* __re
   const uint64_t end = S.max_steps < (uint64_t)cap ? S.max_steps : (uint64_t)cap;
   uint64_t i = 1;
   double h = S.step_size;
+  double r_prev = 0.0;
+  uint32_t key = 0;
+  bool escaped = false;
   for (; i < end; ++i) {  // identical decisions in the quad's four lanes
     double h_cur = rclamp(h, H_MIN, H_MAX), h_next = 0.0, yn[8];
     int retries = 0, ctl;
@@ -2835,9 +2861,10 @@ __global__ void __launch_bounds__(256, 2) probe_quad_kernel(const DevScene* __re
     double cc[3];
     bool c_valid = false;
     if (should_stop<G>(S, y, cc, c_valid, i) != GRT_STOP_NONE) break;
+    if ((escaped = probe_escaped<G>(S, y, r_prev, cap, &key))) break;
   }
-  uint32_t key = (uint32_t)i;
-  if (i >= end) {
+  if (!escaped) key = (uint32_t)i;
+  if (!escaped && i >= end) {
     key = cap;
     if (S.has_horizon && S.horizon_r > 0.0) {
       const double d = (sqrt(ks_r_sqr(S.a, y[1], y[2], y[3])) - S.horizon_r) / S.horizon_r * 1073741824.0;
