@@ -480,12 +480,16 @@ grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_
   return wl;
 }
 
-// Step cap of the probe rays: an escaping ray needs about max_radius accepted steps at
-// H_MAX = 1 (C4: 15825-15900 steps for max_radius 15000), so 1.3 x max_radius still
-// tells them from the long rays while the capped probes (which run the whole cap) end
-// sooner: C4's probe pass 1.86 s -> ~1.2 s per 1/8 shard.  Scheduling only.
+// Step cap of the probe rays (scheduling only).  The pass lasts as long as its capped
+// probes (horizon creepers) take to run the cap.  An escaping ray needs about max_radius
+// accepted steps at H_MAX = 1 (C4: 15825-15900 for max_radius 15000); round 4 capped at
+// 1.3 x max_radius to tell them from the long rays.  Since round 5 a Kerr-Schild probe
+// moving outward far from the hole ends at once with a key just below the cap
+// (probe_escaped), so the cap no longer has to outlast the escaping rays: 0.3 x
+// max_radius (C4: 4,500 steps; C4 shard 2 0.51 -> 0.09 s before the integrate kernel,
+// the integrate kernel's own time unchanged, profiles/r05aj, r05ak).
 #ifndef GRT_PROBE_CAP_SCALE
-#define GRT_PROBE_CAP_SCALE 1.3
+#define GRT_PROBE_CAP_SCALE 0.3
 #endif
 static uint32_t probe_cap(const grt_scene* s) {
   const double c = GRT_PROBE_CAP_SCALE * s->desc.max_radius;

@@ -2754,18 +2754,20 @@ hipError_t launch_health(int geometry, const DevScene* d_scene, const WorkList& 
 // probe pixel's own count; the 300 tiles with a ray past 8e5 steps are among the 311
 // largest keys but 11; tools/c4_probe_features.py), so the longest tiles are queued first.
 #ifndef GRT_PROBE_ESCAPE
-#define GRT_PROBE_ESCAPE 0  // experiment: end an outward-bound probe beyond 10 radii early
+#define GRT_PROBE_ESCAPE 1  // end an outward-bound Kerr-Schild probe far from the hole at once
 #endif
-// Experiment (GRT_PROBE_ESCAPE, Kerr-Schild): a probe moving outward beyond 10 horizon
-// scales escapes; its key becomes cap - 1 (below every capped probe's, as its ray is
-// shorter than theirs), so a cap below the escaping rays' length still ranks them.
+// A Kerr-Schild probe moving outward beyond min(10 radius, max_radius / 2) escapes (no
+// turning point outside the photon orbits); its key becomes cap - 1: below every capped
+// probe's key (those rays are longer), above the rays that fell in early, and "finished"
+// for the edge-tile rule (schedule.hip).  So the cap (api.hip probe_cap) need not outlast
+// the escaping rays, and the pass ends sooner.  Scheduling only, never an output.
 template <int G>
 GDEV bool probe_escaped(const DevScene& S, const double* y, double& r_prev, uint32_t cap, uint32_t* key) {
   if constexpr (G != GRT_GEOM_KERR || !GRT_PROBE_ESCAPE) {
     return false;
   } else {
     const double r = sqrt(ks_r_sqr(S.a, y[1], y[2], y[3]));
-    const bool out = r > 10.0 * S.radius && r > r_prev;
+    const bool out = r > fmin(10.0 * S.radius, 0.5 * sqrt(S.max_radius_sq)) && r > r_prev;
     r_prev = r;
     if (out) *key = cap - 1;
     return out;
