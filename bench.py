@@ -306,8 +306,8 @@ def run_c2(args, rank, world, local_rank, dev):
     # frame in flight, the mean launch duration)
     if F == 1:
         kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    else:
-        kernel_ms = ev[0][0].elapsed_time(ev[-1][1]) / args.steps
+    else:  # the last frame to finish is one of the last F
+        kernel_ms = max(ev[0][0].elapsed_time(e[1]) for e in ev[-F:]) / args.steps
     counters = [sum(v) for v in zip(*(s["stats"].cpu().tolist() for s in slots))]
     accepted, attempts = counters[0], counters[1]  # summed over K frames
 
