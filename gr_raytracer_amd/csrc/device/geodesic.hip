@@ -2154,8 +2154,14 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         }
       }
       w_rays += __popcll(__ballot(fresh));
+#ifndef GRT_TAIL_PRIO_BL
+#define GRT_TAIL_PRIO_BL 0  // experiment: the same for KerrBL, with len = GRT_TAIL_PRIO_BL_LEN accepted steps
+#endif
+#ifndef GRT_TAIL_PRIO_BL_LEN
+#define GRT_TAIL_PRIO_BL_LEN 1200.0
+#endif
 #if GRT_TAIL_PRIO
-      if constexpr (!TAIL && G != GRT_GEOM_KERR_BL) {  // KerrBL's rays are all short
+      if constexpr (!TAIL && (G != GRT_GEOM_KERR_BL || GRT_TAIL_PRIO_BL)) {  // KerrBL's rays are all short
         // After the queue has drained for this wave (one of its lanes found no item), the
         // pass ends on the rays with the most steps left, so the waves holding them get the
         // SIMD's issue slots first (s_setprio; the arbiter otherwise serves the oldest wave):
@@ -2165,7 +2171,8 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
           uint32_t mi = active ? (uint32_t)i : 0xffffffffu;
 #pragma unroll
           for (int off = 32; off > 0; off >>= 1) mi = min(mi, (uint32_t)__shfl_xor((int)mi, off));
-          const double len = sqrt(S.max_radius_sq), left = len - (double)mi;
+          const double len = G == GRT_GEOM_KERR_BL ? GRT_TAIL_PRIO_BL_LEN : sqrt(S.max_radius_sq);
+          const double left = len - (double)mi;
           if (left > 0.67 * len) __builtin_amdgcn_s_setprio(3);
           else if (left > 0.33 * len) __builtin_amdgcn_s_setprio(2);
           else __builtin_amdgcn_s_setprio(1);

@@ -1,9 +1,9 @@
 """Per-ray schedule of one integrate launch from a diagnostic build (tools/build_variant.sh
-rt 's/x/x/' -DGRT_RAY_TIMES=1, loaded through GRT_LIB): C2's whole frame (c2) or C5's
-supersample pass (c5: trace 2 of grt_render_section).  Prints the live-ray count over
+rt 's/x/x/' -DGRT_RAY_TIMES=1, loaded through GRT_LIB): C2's whole frame (c2), C3's (c3:
+kerr-bl.toml, the C3 camera) or C5's supersample pass (c5: trace 2 of grt_render_section).  Prints the live-ray count over
 time, the time the queue drained (last ray start), the kernel's end and the lane
 occupancy (live-ray time over lanes x span); saves start / end / attempts to OUT.npz.
-usage: python tools/ray_timeline.py c2|c5 OUT.npz"""
+usage: python tools/ray_timeline.py c2|c3|c5 OUT.npz"""
 import ctypes as C
 import json
 import sys
@@ -20,8 +20,12 @@ if "GRT_BLOCKS_PER_CU" in os.environ:  # integrate-kernel blocks per CU (default
 from gr_raytracer_amd import _lib as L  # noqa: E402
 
 mode, out = sys.argv[1], sys.argv[2]
-opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, max_steps=100000)
-hs = g.HostScene(str(ROOT / "tests/golden/scenes/schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
+if mode == "c3":
+    opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-10.0, 0.0, -0.5), theta=-3.14159, max_steps=1000000)
+    hs = g.HostScene(str(ROOT / "tests/golden/scenes/kerr-bl.toml"), opts, str(ROOT / "tests/golden"))
+else:
+    opts = g.GlobalOpts(width=1500, height=1500, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, max_steps=100000)
+    hs = g.HostScene(str(ROOT / "tests/golden/scenes/schwarzschild.toml"), opts, str(ROOT / "tests/golden"))
 lib = L.lib()
 only = lib.grt_debug_ray_times_only
 only.argtypes = [C.c_uint64]
