@@ -240,6 +240,36 @@ def reduce_over_ranks(elapsed: float, accepted: float, attempts: float, world: i
     return float(t[0]), float(t[1]), float(t[2])
 
 
+def c2_frame_loop(n_slots: int, steps: int, warmup: int, render, gather, sync, barrier, reset, record=None) -> float:
+    """The C2 weak-scaling loop, backend-agnostic (RCCL streams on the GPUs, gloo in tests).
+    Frame k goes to slot k mod n_slots: render(slot) enqueues it, gather(slot) (or None)
+    sends it to rank 0, record(k, 0 | 1, slot) brackets the render for the device events.
+    A warm-up step renders one frame in every slot; reset() then clears the counters.
+    Returns the timed region's wall time (barrier and sync on both sides)."""
+    for _ in range(warmup):
+        for j in range(n_slots):
+            render(j)
+            if gather is not None:
+                gather(j)
+    sync()
+    reset()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        j = k % n_slots
+        if record is not None:
+            record(k, 0, j)
+        render(j)
+        if record is not None:
+            record(k, 1, j)
+        if gather is not None:
+            gather(j)
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
 def run_c2(args, rank, world, local_rank, dev):
     import torch
     import torch.distributed as dist
@@ -270,38 +300,25 @@ def run_c2(args, rank, world, local_rank, dev):
             if (gathered and rank == 0) else None,
         })
 
-    def one_step(k, ev=None):
-        s = slots[k % F]
-        st = s["stream"]
-        if ev is not None:
-            ev[0].record(st)
-        L.check(lib.grt_render_pixels_async(s["scene"]._s, local_rank, st.cuda_stream, 0, 0, rows, cols,
+    def render(j):
+        s = slots[j]
+        L.check(lib.grt_render_pixels_async(s["scene"]._s, local_rank, s["stream"].cuda_stream, 0, 0, rows, cols,
                                             s["xyza"].data_ptr(), s["cls"].data_ptr(), s["status"].data_ptr(),
                                             None, None, None, s["stats"].data_ptr()), "grt_render_pixels_async")
-        if ev is not None:
-            ev[1].record(st)
-        if gathered:  # on the slot's stream: the gather waits for this frame only, and the
-            with torch.cuda.stream(st):  # slot's next frame waits for the gather
-                dist.gather(s["xyza"], gather_list=s["gather"], dst=0, async_op=True).wait()
 
-    for _ in range(args.warmup):  # a warm-up step renders one frame in every slot
-        for j in range(F):
-            one_step(j)
-    torch.cuda.synchronize(dev)
+    def gather(j):  # on the slot's stream: the gather waits for this frame only, and the
+        s = slots[j]  # slot's next frame waits for the gather
+        with torch.cuda.stream(s["stream"]):
+            dist.gather(s["xyza"], gather_list=s["gather"], dst=0, async_op=True).wait()
 
-    for s in slots:
-        s["stats"].zero_()
+    def reset():
+        for s in slots:
+            s["stats"].zero_()
+
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(k, ev[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = c2_frame_loop(F, args.steps, args.warmup, render, gather if gathered else None,
+                            lambda: torch.cuda.synchronize(dev), (lambda: dist.barrier()) if world > 1 else (lambda: None),
+                            reset, lambda k, e, j: ev[k][e].record(slots[j]["stream"]))
     # the device time per frame: first frame's start to last frame's end over K (with one
     # frame in flight, the mean launch duration)
     if F == 1:

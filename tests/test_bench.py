@@ -1,6 +1,7 @@
 """bench.py's host logic on CPU: the C4 strong-scaling loop over gloo (world 2, and world 8
-with 16-row cyclic bands: the north-star layout), the
-host-core census, and the roofline's refusal of a PMC summary from another build.
+with 16-row cyclic bands: the north-star layout), the C2 weak-scaling loop with two frames
+in flight over gloo (world 2), the host-core census, and the roofline's refusal of a PMC
+summary from another build.
 
 The C4 loop (bench.c4_frame_steps / c4_summary) is backend-agnostic; here each rank's
 shard trace is the oracle (this container has no GPU), at a reduced frame size.  The
@@ -175,3 +176,58 @@ def test_weak_scaling_totals_gloo_world2():
     import bench
 
     assert list(bench.reduce_over_ranks(1.5, 7.0, 8.0, 1)) == [1.5, 7.0, 8.0]
+
+
+def _c2_loop_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n_slots, steps, warmup = 2, 5, 1
+        bufs = [torch.zeros(4) for _ in range(n_slots)]
+        lists = [[torch.zeros(4) for _ in range(world)] for _ in range(n_slots)] if rank == 0 else None
+        seq, log = [0], []
+
+        def render(j):  # frame number `seq` of this rank into slot j
+            bufs[j].fill_(100.0 * rank + seq[0])
+            log.append(("render", j, seq[0]))
+            seq[0] += 1
+
+        def gather(j):
+            dist.gather(bufs[j], gather_list=lists[j] if rank == 0 else None, dst=0)
+
+        elapsed = bench.c2_frame_loop(n_slots, steps, warmup, render, gather, lambda: None, dist.barrier,
+                                      lambda: log.append(("reset",)), lambda k, e, j: log.append(("ev", k, e, j)))
+        out = {"elapsed": elapsed, "log": log,
+               "gathered": [[float(t[0]) for t in lists[j]] for j in range(n_slots)] if rank == 0 else None}
+        with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+            json.dump(out, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c2_frame_loop_gloo_world2():
+    """bench.c2_frame_loop (the C2 weak-scaling loop with two frames in flight) over gloo,
+    world 2: a warm-up step renders one frame per slot, the counters are reset once, frame
+    k goes to slot k mod 2 bracketed by its two events, and each frame is gathered to rank
+    0 from its slot, so rank 0 ends with every rank's last frame of each slot."""
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_c2_loop_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        got = [json.load(open(os.path.join(d, f"r{r}.json"))) for r in range(2)]
+    for r in range(2):
+        log = [tuple(e) for e in got[r]["log"]]
+        assert log[:3] == [("render", 0, 0), ("render", 1, 1), ("reset",)]
+        timed = log[3:]
+        assert len(timed) == 5 * 3
+        for k in range(5):
+            assert timed[3 * k:3 * k + 3] == [("ev", k, 0, k % 2), ("render", k % 2, 2 + k), ("ev", k, 1, k % 2)]
+        assert got[r]["elapsed"] > 0.0
+    # slot 0's last frame is number 6 (timed k = 4), slot 1's number 5 (k = 3), from each rank
+    assert got[0]["gathered"] == [[6.0, 106.0], [5.0, 105.0]]
