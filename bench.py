@@ -357,9 +357,6 @@ def run_c2(args, rank, world, local_rank, dev):
         f"device time per frame with {F} frames in flight: first frame's start event to last frame's end event "
         f"/ K (HIP events on the slots' streams); a single launch's duration overlaps its neighbours' "
         f"(rocprof: the spacing of consecutive integrate-kernel ends, tools/kernel_period.py)")
-    # each launch's own start-to-end span (with F > 1 it includes the overlap with its
-    # neighbours, as rocprof's per-kernel average does)
-    line["roofline"]["launch_ms_mean"] = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(g, "c2")
     return line
