@@ -70,6 +70,9 @@ namespace grt {
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
+#ifndef GRT_CLAIM_REFRESH
+#define GRT_CLAIM_REFRESH 0  // experiment: KerrBL reads the work counter before a chunk claim
+#endif
 #ifndef GRT_TAIL_PRIO
 #define GRT_TAIL_PRIO 1  // light charts: issue priority by steps left once the queue drains (C5 -1.2%, profiles/r05i)
 #endif
@@ -2084,8 +2087,18 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       // worth of lanes of the end: its 2.25M short rays end ~13M times a second, and an
       // atomic on one address per refill cost C3 +16% (profiles/r05l, r05m).
       const uint64_t grid_lanes = (uint64_t)gridDim.x * blockDim.x;
-      const bool exact =
-          TAIL || two_ended || G != GRT_GEOM_KERR_BL || chunk_end + 2 * grid_lanes >= n_items;
+      bool exact = TAIL || two_ended || G != GRT_GEOM_KERR_BL || chunk_end + 2 * grid_lanes >= n_items;
+#if GRT_CLAIM_REFRESH
+      if (!exact && cnt > remaining) {
+        // the wave's view (its last chunk's end) is old when its lanes ran slowly: before a
+        // chunk claim, read the counter, so that a wave the arbiter served last does not
+        // take 64 items near the end of the queue and start them one ray lifetime late
+        unsigned long long c0 = 0;
+        if (lane == 0) c0 = load_agent(counter);
+        c0 = __shfl(c0, 0);
+        exact = c0 + 2 * grid_lanes >= n_items;
+      }
+#endif
       const uint64_t take = exact ? cnt - remaining : CHUNK;
       if (cnt > remaining) {
         unsigned long long b = 0;
