@@ -24,6 +24,12 @@ gather time.  A 4096^2 frame takes minutes per GPU: run it with --steps 1 --warm
 Printed JSON carries the FP64 VALU roofline of the trace kernel (HIP events on the launch
 stream) and the CPU baseline: the oracle (reference algorithm restated in C++, stored
 trajectories + post-hoc window pass) timed on the host cores on a bounded sample.
+
+The metric's second half, "wall-clock for 1500x1500 Schwarzschild render", is the
+reference's own Elapsed time (main.rs:31, :175-176: CLI start -> image written): on one GPU
+the C2 line also runs the `grt` CLI (the reference's `render` command line, README.md:63)
+on the C2 scene at 1 spp and on the stock TOML (adaptive 4x4 supersampling, C5) and
+reports the process wall time and the CLI's phase times (render_wall).
 """
 from __future__ import annotations
 
@@ -240,6 +246,66 @@ def reduce_over_ranks(elapsed: float, accepted: float, attempts: float, world: i
     return float(t[0]), float(t[1]), float(t[2])
 
 
+# ---------------------------------------------------------------- CLI wall ----
+README_FLAGS = ["--width=1500", "--height=1500", "--camera-position=-16.0,0.0,3.5", "--theta=-3.142", "--psi=0.0",
+                "--phi=0.0", "--max-steps=100000"]  # README.md:63, BASELINE configs[1]
+
+
+def parse_cli_phases(stderr: str) -> dict:
+    """The `[grt] phases (ms): load L, create C, render R, output O, write W, since start S`
+    line and the reference's `Elapsed time: ...` line of a `grt ... render` run."""
+    import re
+
+    out = {}
+    m = re.search(r"\[grt\] phases \(ms\): (.*)", stderr)
+    if m:
+        for part in m.group(1).split(","):
+            k, v = part.strip().rsplit(" ", 1)
+            out[k.replace(" ", "_") + "_ms"] = float(v)
+    m = re.search(r"INFO Elapsed time: (\S+)", stderr)
+    if m:
+        out["elapsed_line"] = m.group(1)
+    m = re.search(r"\[grt\] (\d+) rays, (\d+) accepted steps", stderr)
+    if m:
+        out["rays"], out["accepted_steps"] = int(m.group(1)), int(m.group(2))
+    return out
+
+
+def cli_wall(adaptive: bool, device: int = 0, reps: int = 2) -> dict:
+    """`grt ... render` on the C2 scene (BASELINE's wall-clock half): process start -> exit
+    with the PNG written, best of `reps` runs (each a fresh process: HIP runtime start, TOML
+    and texture decode, upload, trace, tone map, PNG encode).  adaptive=False renders the
+    1-spp C2 frame (the TOML with [adaptive_sampling] enabled = false, the fixture BASELINE.md
+    names); True the stock TOML, whose default adaptive 4x4 supersampling makes it C5."""
+    import subprocess
+    import tempfile
+
+    exe = ROOT / "gr_raytracer_amd" / "lib" / "grt"
+    with tempfile.TemporaryDirectory() as d:
+        toml = SCENES / "schwarzschild.toml"
+        if not adaptive:
+            toml = Path(d) / "schwarzschild-1spp.toml"
+            toml.write_text((SCENES / "schwarzschild.toml").read_text() + "\n[adaptive_sampling]\nenabled = false\n")
+        png = Path(d) / "render.png"
+        runs = []
+        for _ in range(reps):
+            if png.exists():
+                png.unlink()
+            cmd = [str(exe), *README_FLAGS, "--device", str(device), "--resource-root", str(ROOT / "tests/golden"),
+                   "--config-file", str(toml), "render", "--filename", str(png)]
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            wall = time.perf_counter() - t0
+            if r.returncode != 0 or not png.exists():
+                return {"error": f"grt exited {r.returncode}: {r.stderr[-400:]}"}
+            runs.append((wall, parse_cli_phases(r.stderr)))
+    wall, phases = min(runs, key=lambda x: x[0])
+    return {"render_wall_s": round(wall, 3), "runs_s": [round(w, 3) for w, _ in runs],
+            "command": "grt " + " ".join(README_FLAGS) + f" --config-file {toml.name} render",
+            "scene": "schwarzschild.toml" + ("" if adaptive else " + [adaptive_sampling] enabled = false (1 spp)"),
+            "phases": phases}
+
+
 def c2_frame_loop(n_slots: int, steps: int, warmup: int, render, gather, sync, barrier, reset, record=None) -> float:
     """The C2 weak-scaling loop, backend-agnostic (RCCL streams on the GPUs, gloo in tests).
     Frame k goes to slot k mod n_slots: render(slot) enqueues it, gather(slot) (or None)
@@ -327,6 +393,21 @@ def run_c2(args, rank, world, local_rank, dev):
         kernel_ms = max(ev[0][0].elapsed_time(e[1]) for e in ev[-F:]) / args.steps
     counters = [sum(v) for v in zip(*(s["stats"].cpu().tolist() for s in slots))]
     accepted, attempts = counters[0], counters[1]  # summed over K frames
+    # One frame alone in flight (after the timed region, untimed): a single launch's own
+    # duration, the basis of frac_single_launch beside the pipelined throughput fraction.
+    single_ms = []
+    if args.single_launches > 0:
+        s0 = slots[0]
+        for _ in range(args.single_launches):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0["stats"].zero_()
+            torch.cuda.synchronize(dev)
+            e0.record(s0["stream"])
+            render(0)
+            e1.record(s0["stream"])
+            e1.synchronize()
+            single_ms.append(e0.elapsed_time(e1))
+        single_counts = s0["stats"].cpu().tolist()
 
     elapsed, total_acc, total_att = reduce_over_ranks(elapsed, accepted, attempts, world, dev)
     if rank != 0:
@@ -346,7 +427,9 @@ def run_c2(args, rank, world, local_rank, dev):
                    "steps_per_gpu_per_s": total_acc / elapsed / world,
                    "attempts_per_accepted": total_att / max(total_acc, 1.0),
                    "accepted_steps_per_frame": total_acc / (args.steps * world),
-                   "frame_wall_s_per_gpu": elapsed / args.steps},
+                   # wall time per frame of the timed loop (with F frames in flight: the
+                   # throughput period, not one frame's latency; see single_launch_ms)
+                   "frame_period_s": elapsed / args.steps},
         "roofline": roofline("c2", "schwarzschild", accepted / args.steps, attempts / args.steps, kernel_ms, n,
                              "grt::integrate_kernel<1, false> (Schwarzschild; events also span shade_kernel<1, 0>, "
                              "<0.01%)"),
@@ -354,9 +437,20 @@ def run_c2(args, rank, world, local_rank, dev):
     }
     line["roofline"]["kernel_ms_basis"] = (
         "mean launch duration (HIP events on the launch stream)" if F == 1 else
-        f"device time per frame with {F} frames in flight: first frame's start event to last frame's end event "
-        f"/ K (HIP events on the slots' streams); a single launch's duration overlaps its neighbours' "
-        f"(rocprof: the spacing of consecutive integrate-kernel ends, tools/kernel_period.py)")
+        f"pipelined throughput: device time per frame with {F} frames in flight, first frame's start event to "
+        f"last frame's end event / K (HIP events on the slots' streams); a single launch's duration overlaps its "
+        f"neighbours' (rocprof: the spacing of consecutive integrate-kernel ends, tools/kernel_period.py), so this "
+        f"frac is a throughput fraction; frac_single_launch is one launch's")
+    if single_ms:
+        r1 = roofline("c2", "schwarzschild", single_counts[0], single_counts[1], min(single_ms), n, "")
+        line["roofline"]["single_launch_ms"] = [round(v, 2) for v in single_ms]
+        line["roofline"]["frac_single_launch"] = r1["frac"]
+        line["roofline"]["single_launch_basis"] = (
+            f"{len(single_ms)} frames rendered alone after the timed region (one in flight, slot 0's stream), "
+            f"shortest launch; HIP events around grt_render_pixels_async (integrate + shade kernels)")
+    if world == 1 and not args.no_cli_wall:
+        torch.cuda.synchronize(dev)
+        line["render_wall"] = {"c2_1spp": cli_wall(False, local_rank), "c5_adaptive": cli_wall(True, local_rank)}
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(g, "c2")
     return line
@@ -507,6 +601,9 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=2,
                     help="c2: frames in flight (one stream and workspace each); 1 = one frame after another")
     ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--single-launches", type=int, default=2,
+                    help="c2: frames rendered alone after the timed region (frac_single_launch)")
+    ap.add_argument("--no-cli-wall", action="store_true", help="c2: skip the grt CLI wall-clock runs")
     ap.add_argument("--self-gather", action="store_true", help="c2, one GPU: run the multi-GPU gather path "
                     "in a process group of one (a check of the streams and RCCL gathers)")
     args = ap.parse_args()

@@ -119,6 +119,22 @@ class SubsampleFailures(C.Structure):
                 ("steps", C.POINTER(C.c_uint32))]
 
 
+GRT_MULTI_MAX_DEVICES = 16
+
+
+class FrameOut(C.Structure):
+    """grt_frame_out: host outputs of grt_render_frame_multi, frame order (NULL: not gathered)."""
+    _fields_ = [("xyza", C.POINTER(C.c_float)), ("xyza64", _pd), ("ray_class", C.POINTER(C.c_uint8)),
+                ("status", C.POINTER(C.c_uint8)), ("stop", C.POINTER(C.c_uint8)), ("steps", C.POINTER(C.c_uint32))]
+
+
+class MultiReport(C.Structure):
+    _fields_ = [("n_devices", C.c_uint32), ("record_bytes", C.c_uint32), ("attempts", C.c_uint32),
+                ("_pad", C.c_uint32), ("wall_ms", _d), ("gather_ms", _d), ("allgather_ms", _d),
+                ("trace_ms", _d * GRT_MULTI_MAX_DEVICES), ("accepted_steps", C.c_uint64 * GRT_MULTI_MAX_DEVICES),
+                ("rows", C.c_uint64 * GRT_MULTI_MAX_DEVICES)]
+
+
 class Health(C.Structure):
     _fields_ = [
         ("rays", C.c_uint64), ("failed", C.c_uint64), ("null_violations", C.c_uint64), ("max_null", _d),
@@ -233,6 +249,10 @@ def lib() -> C.CDLL:
         "grt_ray_at": (C.c_int, [i32, _d, _d, _pd, _pd, _pd, _pd]),
         "grt_write_trajectory_csv": (C.c_int, [C.c_char_p, i32, _d, _pd, u64]),
         "grt_format_f64": (C.c_size_t, [_d, C.c_char_p, C.c_size_t]),
+        "grt_render_frame_multi": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int), u32, C.POINTER(AdaptiveConfig), _pd,
+                                             C.POINTER(FrameOut), C.POINTER(C.c_uint64), C.POINTER(Stats),
+                                             C.POINTER(SubsampleFailures), C.POINTER(MultiReport)]),
+        "grt_multi_release": (None, []),
     }
     # GRT_LIB_ALLOW_MISSING=1 (tools/time_variants.py only) binds an older experimental
     # build that lacks newer entry points; by default a missing symbol is an error.
@@ -279,7 +299,7 @@ EXPORTED_SYMBOLS = [
     "grt_linear_max_async", "grt_tonemap_async", "grt_xyz_to_srgb8_device", "grt_trace_pixels", "grt_trace_rays",
     "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_adaptive_min_luminance_device", "grt_supersample_shard",
     "grt_supersample_shard_device", "grt_adaptive_floor_device", "grt_render_section_ex",
-    "grt_write_png_rgb", "grt_write_hdr_xyz",
+    "grt_write_png_rgb", "grt_write_hdr_xyz", "grt_render_frame_multi", "grt_multi_release",
 ]
 
 

@@ -15,7 +15,10 @@
 //
 // Global options go before the subcommand, subcommand options after it (clap).
 // Extra (not in the reference): --device N selects the GPU, --resource-root DIR
-// resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer.
+// resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer; --gpus N (GPUs
+// 0..N-1) or --devices A,B,... renders the whole frame over several GPUs of this process
+// (grt_render_frame_multi: cyclic row bands of --band-rows rows, default 16, one RCCL
+// gather), --gpus 1 included.
 #include <algorithm>
 #include <charconv>
 #include <chrono>
@@ -233,6 +236,8 @@ int main(int argc, char** argv) {
   uint32_t bb_w = 1000, bb_h = 1000;
   bool have_temperature = false;
   int device = 0;
+  std::vector<int> multi_devices;  // --gpus / --devices: the multi-GPU frame
+  uint32_t band_rows = 16;
   std::vector<std::string> args(argv + 1, argv + argc);
   for (size_t i = 0; i < args.size(); ++i) {
     std::string a = args[i], val;
@@ -267,6 +272,27 @@ int main(int argc, char** argv) {
     long long iv = 0;
     // extras accepted anywhere
     if (a == "--device") { device = std::atoi(v.c_str()); continue; }
+    if (a == "--gpus") {
+      if (!int_in(1, GRT_MULTI_MAX_DEVICES, &iv)) return bad();
+      multi_devices.clear();
+      for (long long k = 0; k < iv; ++k) multi_devices.push_back((int)k);
+      continue;
+    }
+    if (a == "--devices") {
+      std::vector<double> ds;
+      if (!split_csv(v, ds) || ds.empty() || ds.size() > GRT_MULTI_MAX_DEVICES) return bad();
+      multi_devices.clear();
+      for (double x : ds) {
+        if (x < 0 || x != (double)(int)x) return bad();
+        multi_devices.push_back((int)x);
+      }
+      continue;
+    }
+    if (a == "--band-rows") {
+      if (!int_in(1, 4294967295ull, &iv)) return bad();
+      band_rows = (uint32_t)iv;
+      continue;
+    }
     if (a == "--resource-root") { resource_root = v; continue; }
     if (a == "--raw-out") { raw_out = v; continue; }
     if (!action.empty()) {  // subcommand options
@@ -376,6 +402,11 @@ int main(int argc, char** argv) {
     filename = action == "render" ? "render.png" : (action == "render-ray" ? "rendered-ray.csv" : "rendered-ray-at.csv");
   if (config_file.empty()) return usage("Config file is required for this action");
 
+  // phase times of a render (printed on one [grt] line at the end; not in the reference)
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  double ph_load = 0, ph_create = 0, ph_render = 0, ph_output = 0, ph_write = 0;
+  auto t_phase = clk::now();
   grt_host_scene* hs = nullptr;
   if (action == "render-ray-at" ? grt_host_geometry_load(config_file.c_str(), &opts, &hs)
                                 : grt_host_scene_load(config_file.c_str(),
@@ -386,11 +417,14 @@ int main(int argc, char** argv) {
   }
   grt_adaptive_config ac;
   grt_host_scene_adaptive(hs, &ac);
+  ph_load = ms_since(t_phase);
+  t_phase = clk::now();
   grt_scene* scene = nullptr;
   if (grt_scene_create(grt_host_scene_desc(hs), &scene)) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
+  ph_create = ms_since(t_phase);
   const grt_scene_desc* d = grt_host_scene_desc(hs);
   auto elapsed = [&]() {  // main.rs:175-176
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
@@ -465,14 +499,29 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "[grt] INFO Tone mapping method: %s\n",
                  opts.tone_mapping == GRT_TONE_GLOBAL_LINEAR ? "GlobalLinear" : "Reinhard");
   }
+  const bool multi = !multi_devices.empty();
+  if (multi && (r0 != 0 || c0 != 0 || r1 != (uint32_t)opts.height || c1 != (uint32_t)opts.width))
+    return usage("--gpus / --devices render whole frames (no --from-row/--from-col/--to-row/--to-col)");
   if (supersampled)  // raytracer.rs:264-267
     std::fprintf(stderr, "[grt] INFO Rendering section from (%u, %u) to (%u, %u) with supersampling\n", r0, c0, r1,
                  c1);
-  if (grt_render_section_ex(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st,
-                            status.data(), &fails, stop.data(), steps.data())) {
+  t_phase = clk::now();
+  grt_multi_report mrep;
+  if (multi) {
+    // the frame over several GPUs: cyclic row bands, one host thread per device, one RCCL
+    // gather of f64 XYZA + class + status + stop + steps (39 B per pixel) to the first
+    grt_frame_out fo{nullptr, xyza.data(), nullptr, status.data(), stop.data(), steps.data()};
+    if (grt_render_frame_multi(scene, (int)multi_devices.size(), multi_devices.data(), band_rows, &ac, maskp, &fo,
+                               &nsel, &st, &fails, &mrep)) {
+      std::fprintf(stderr, "Error: %s\n", grt_last_error());
+      return 1;
+    }
+  } else if (grt_render_section_ex(scene, device, r0, c0, r1, c1, &ac, maskp, xyza.data(), nullptr, &nsel, &st,
+                                   status.data(), &fails, stop.data(), steps.data())) {
     std::fprintf(stderr, "Error: %s\n", grt_last_error());
     return 1;
   }
+  ph_render = ms_since(t_phase);
   // The 1-spp pass, in pixel order (the reference logs from its parallel loop):
   //  * raytracer.rs:232-239: a pixel whose color_of_ray failed (Debug form of the
   //    RaytracerError); it keeps the default colour;
@@ -507,12 +556,24 @@ int main(int argc, char** argv) {
                "(%.3e steps/s)\n",
                (unsigned long long)st.rays, (unsigned long long)st.accepted_steps, (unsigned long long)st.attempts,
                (unsigned long long)nsel, st.kernel_ms, st.accepted_steps / (st.kernel_ms * 1e-3));
+  if (multi) {
+    std::string per;
+    for (uint32_t k = 0; k < mrep.n_devices; ++k) {
+      char b[96];
+      std::snprintf(b, sizeof(b), "%s%d: %llu rows %.1f ms", k ? ", " : "", multi_devices[k],
+                    (unsigned long long)mrep.rows[k], mrep.trace_ms[k]);
+      per += b;
+    }
+    std::fprintf(stderr, "[grt] %u GPU(s) [%s]; allgather %.2f ms, gather %.2f ms (%u B per pixel), %u trace(s)\n",
+                 mrep.n_devices, per.c_str(), mrep.allgather_ms, mrep.gather_ms, mrep.record_bytes, mrep.attempts);
+  }
   if (st.march_jobs)
     std::fprintf(stderr, "[grt] VolumetricDisc: %llu raymarches, %llu samples (%llu with noise, %llu emitting)\n",
                  (unsigned long long)st.march_jobs, (unsigned long long)st.march_samples,
                  (unsigned long long)st.march_noise_samples, (unsigned long long)st.march_emit_samples);
   std::string err;
   bool ok;
+  t_phase = clk::now();
   if (hdr) {
     std::vector<float> rgb((size_t)w * h * 3);
     for (size_t i = 0; i < (size_t)w * h; ++i)
@@ -522,10 +583,13 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> rgb((size_t)w * h * 3);
     // output stage on the GPU (color.rs:204-298 via output.hip), exposure 1 as in
     // render_section (raytracer.rs:485)
-    if (grt_xyz_to_srgb8_device(device, xyza.data(), (size_t)w * h, opts.tone_mapping, 1.0, rgb.data())) {
+    if (grt_xyz_to_srgb8_device(multi ? multi_devices[0] : device, xyza.data(), (size_t)w * h, opts.tone_mapping,
+                                1.0, rgb.data())) {
       std::fprintf(stderr, "Error: %s\n", grt_last_error());
       return 1;
     }
+    ph_output = ms_since(t_phase);
+    t_phase = clk::now();
     ok = grt_host::png_encode_rgb(filename, rgb.data(), w, h, err);
   }
   if (!ok) {
@@ -539,9 +603,15 @@ int main(int argc, char** argv) {
       std::fclose(f);
     }
   }
+  ph_write = ms_since(t_phase);
+  if (multi) grt_multi_release();
   grt_scene_destroy(scene);
   grt_host_scene_destroy(hs);
   std::fprintf(stderr, "[grt] INFO saved image to %s\n", filename.c_str());  // raytracer.rs:494
+  // where the wall time went: TOML + texture decode + LUTs; the descriptor copy; the render
+  // call (device upload on first use, trace, supersampling, D2H); tone map; encode + write
+  std::fprintf(stderr, "[grt] phases (ms): load %.1f, create %.1f, render %.1f, output %.1f, write %.1f, "
+               "since start %.1f\n", ph_load, ph_create, ph_render, ph_output, ph_write, ms_since(t_start));
   elapsed();
   return 0;
 }

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <climits>
 #include <cmath>
@@ -24,14 +25,26 @@
 
 namespace {
 
-int g_blocks_per_cu = 0;
-int g_range_free = 1;  // grt_debug_range_free: 0 = every division and sqrt in its IEEE form (tests)
-int g_threads = 256;
-int g_probe_quad = -1;  // Kerr-Schild probe on quads: -1 auto, 0 never, 1 always (grt_debug_probe_keys)
-int g_schedule = -1;  // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
-int g_two_ended = 1;  // grt_set_two_ended: probe-ordered traces take the queue from both ends
-long long g_tail = -1;  // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
+// Process-wide tuning knobs (grt_set_*).  The library is called from one host thread per
+// device (grt_render_frame_multi, or a host of its own), so a setter may run beside renders
+// on other threads: the knobs are atomics, and a trace reads them once, into a Knobs
+// snapshot, so that one call never sees two settings.
+std::atomic<long long> g_launch{256};  // grt_set_launch_config: blocks per CU << 16 | threads per block
+std::atomic<int> g_range_free{1};      // grt_debug_range_free: 0 = every division and sqrt in its IEEE form (tests)
+std::atomic<int> g_schedule{-1};       // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
+std::atomic<int> g_two_ended{1};       // grt_set_two_ended: probe-ordered traces take the queue from both ends
+std::atomic<long long> g_tail{-1};     // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
 constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
+
+struct Knobs {
+  int blocks_per_cu, threads, schedule, two_ended;
+  long long tail;
+  static Knobs now() {
+    const long long l = g_launch.load(std::memory_order_relaxed);
+    return Knobs{(int)(l >> 16), (int)(l & 0xffff), g_schedule.load(std::memory_order_relaxed),
+                 g_two_ended.load(std::memory_order_relaxed), g_tail.load(std::memory_order_relaxed)};
+  }
+};
 
 
 int fail(int code, const std::string& msg) {
@@ -52,7 +65,7 @@ struct HostTexture {
 };
 
 struct DeviceCopy {
-  bool ready = false;
+  std::atomic<bool> ready{false};  // set (release) once the device copy below is complete
   grt::DevScene* d_scene = nullptr;
   std::vector<void*> allocations;
   unsigned long long* d_counter = nullptr;  // [0] work counter, [5..6] hit pool (HitPool::count)
@@ -93,12 +106,12 @@ struct DeviceCopy {
 
 constexpr uint64_t POOL_MIN = 1ull << 20;            // records
 constexpr uint64_t POOL_MAX = (1ull << 31) - 1;      // job and list encodings hold 31 bits
-uint64_t g_pool_min = POOL_MIN;                      // grt_set_hit_pool_min (tests force a full pool)
+std::atomic<uint64_t> g_pool_min{POOL_MIN};         // grt_set_hit_pool_min (tests force a full pool)
 uint64_t pool_record_bytes(bool vol) { return 4 + 1 + 4 * 8 + 3 * 8 + 4 + 4 * 8 + 4 + (vol ? 3 * 8 + 4 * 8 : 0); }
 
 // Grow the hit pool to at least `want` records (never shrinks).
 int ensure_pool(DeviceCopy& dc, uint64_t want) {
-  want = std::min(std::max(want, g_pool_min), POOL_MAX);
+  want = std::min(std::max(want, g_pool_min.load(std::memory_order_relaxed)), POOL_MAX);
   if (want <= dc.pool_cap && dc.pool_mem && (!dc.vol || dc.pool_vol)) return 0;
   want = std::max(want, dc.pool_cap);
   if (dc.pool_mem) {
@@ -224,7 +237,12 @@ struct grt_scene {
   HostTexture obj_tex[GRT_MAX_OBJECTS];
   std::vector<double> lut_r[GRT_MAX_OBJECTS], lut_t[GRT_MAX_OBJECTS];
   std::vector<double> bb_log_t, bb_xyz;
-  std::vector<DeviceCopy*> devices;
+  // one device copy per GPU, created on first use (ensure_device).  Fixed slots, so that a
+  // host thread looking up its device never sees the table move under it while another
+  // thread creates a copy for its own device.
+  static constexpr int MAX_DEVICES = 64;
+  std::atomic<DeviceCopy*> devices[MAX_DEVICES] = {};
+  std::mutex mu;  // creation of the slots' copies
 };
 
 namespace {
@@ -263,15 +281,40 @@ void fill_dev_texture(const grt_texture_desc& t, grt::DevTexture& d) {
   }
 }
 
+int init_device_copy(grt_scene* s, int device, DeviceCopy& dc);
+
+// The scene's copy on `device`, uploaded on first use.  Safe from one host thread per device
+// (and from several threads on one device: the first uploads, the others wait for it).
 int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(-ENODEV, "invalid device ordinal");
-  if ((int)s->devices.size() < ndev) s->devices.resize(ndev, nullptr);
-  if (!s->devices[device]) s->devices[device] = new DeviceCopy();
-  DeviceCopy& dc = *s->devices[device];
+  if (device >= grt_scene::MAX_DEVICES) return fail(-ENODEV, "device ordinal beyond the library's 64 slots");
+  DeviceCopy* p = s->devices[device].load(std::memory_order_acquire);
+  if (!p) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    p = s->devices[device].load(std::memory_order_acquire);
+    if (!p) {
+      p = new DeviceCopy();
+      s->devices[device].store(p, std::memory_order_release);
+    }
+  }
+  DeviceCopy& dc = *p;
   *out = &dc;
-  if (dc.ready) return 0;
+  if (dc.ready.load(std::memory_order_acquire)) return 0;
+  std::lock_guard<std::mutex> lk(dc.mu);
+  if (dc.ready.load(std::memory_order_acquire)) return 0;
+  return init_device_copy(s, device, dc);
+}
+
+// The device copy of a scene on `device` if one is complete, else nullptr.
+DeviceCopy* find_device(const grt_scene* s, int device) {
+  if (device < 0 || device >= grt_scene::MAX_DEVICES) return nullptr;
+  DeviceCopy* p = s->devices[device].load(std::memory_order_acquire);
+  return (p && p->ready.load(std::memory_order_acquire)) ? p : nullptr;
+}
+
+int init_device_copy(grt_scene* s, int device, DeviceCopy& dc) {
   HIP_TRY(hipSetDevice(device));
   const grt_scene_desc& d = s->desc;
   grt::DevScene ds;
@@ -317,7 +360,7 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
     const int lim = d.geometry == GRT_GEOM_KERR ? 20 : 50;
     const bool a_mod = std::fpclassify(d.a) == FP_NORMAL && ea > -lim && ea < lim;
     const bool a_ok = d.geometry == GRT_GEOM_KERR_BL ? a_mod : (d.geometry != GRT_GEOM_KERR || a_mod || d.a == 0.0);
-    ds.div_fast = (g_range_free && std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -lim && ex < lim &&
+    ds.div_fast = (g_range_free.load(std::memory_order_relaxed) && std::fpclassify(d.radius) == FP_NORMAL && d.radius > 0.0 && ex > -lim && ex < lim &&
                    a_ok) ? 1 : 0;
     // ks_fd_ok's coordinate bound: 2^ceil(log2(2 max_radius)) covers every state of a ray
     // (it stops one step beyond max_radius), within the proven 2^10 .. 2^32
@@ -463,7 +506,7 @@ int ensure_device(grt_scene* s, int device, DeviceCopy** out) {
   HIP_TRY(hipEventCreate(&dc.ev1));
   HIP_TRY(hipEventCreateWithFlags(&dc.ev_busy, hipEventDisableTiming));
   (void)occ;
-  dc.ready = true;
+  dc.ready.store(true, std::memory_order_release);
   return 0;
 }
 
@@ -482,17 +525,17 @@ grt::WorkList rect_worklist(uint32_t row0, uint32_t col0, uint32_t rows, uint32_
 
 // Step cap of the probe rays (scheduling only).  The pass lasts as long as its capped
 // probes (horizon creepers) take to run the cap.  An escaping ray needs about max_radius
-// accepted steps at H_MAX = 1 (C4: 15825-15900 for max_radius 15000); round 4 capped at
-// 1.3 x max_radius to tell them from the long rays.  Since round 5 a Kerr-Schild probe
-// moving outward far from the hole ends at once with a key just below the cap
-// (probe_escaped), so the cap no longer has to outlast the escaping rays: 0.3 x
-// max_radius (C4: 4,500 steps; C4 shard 2 0.51 -> 0.09 s before the integrate kernel,
-// the integrate kernel's own time unchanged, profiles/r05aj, r05ak).
-#ifndef GRT_PROBE_CAP_SCALE
-#define GRT_PROBE_CAP_SCALE 0.3
-#endif
+// accepted steps at H_MAX = 1 (C4: 15825-15900 for max_radius 15000), so the cap is
+// 1.3 x max_radius, which tells them from the long rays.  A Kerr-Schild probe moving
+// outward far from the hole ends at once with a key just below the cap (probe_escaped,
+// round 5), so for Kerr-Schild the cap no longer has to outlast the escaping rays:
+// 0.3 x max_radius (C4: 4,500 steps; C4 shard 2 0.51 -> 0.09 s before the integrate
+// kernel, the integrate kernel's own time unchanged, profiles/r05aj, r05ak).  The other
+// charts have no such shortcut and keep 1.3 x: with the short cap their escaping probes
+// would end capped, keyed by their distance to the horizon, ahead of the long rays.
 static uint32_t probe_cap(const grt_scene* s) {
-  const double c = GRT_PROBE_CAP_SCALE * s->desc.max_radius;
+  const double scale = s->desc.geometry == GRT_GEOM_KERR ? 0.3 : 1.3;
+  const double c = scale * s->desc.max_radius;
   return c >= (double)PROBE_CAP ? PROBE_CAP : (c <= 4096.0 ? 4096u : (uint32_t)c);
 }
 
@@ -501,18 +544,19 @@ static uint32_t probe_cap(const grt_scene* s) {
 // in the affine-parameter charts.  KerrBL integrates in Mino time, where even captured
 // rays take ~1e3 steps (C3: max 1147), and Euclidean rays are straight lines: there the
 // probe pass is pure overhead (measured +5% on C3), so automatic mode skips them.
-bool schedule_wanted(const grt_scene* s, const grt::WorkList& wl) {
-  if (wl.pixel_index || g_schedule == 0) return false;
+bool schedule_wanted(const grt_scene* s, const grt::WorkList& wl, const Knobs& k) {
+  if (wl.pixel_index || k.schedule == 0) return false;
   const uint64_t tiles = wl.n_items / 64;
-  if (g_schedule == 1) return tiles > 1;
+  if (k.schedule == 1) return tiles > 1;
   const int g = s->desc.geometry;
   return (g == GRT_GEOM_KERR || g == GRT_GEOM_SCHWARZSCHILD) && s->desc.max_steps >= 8ull * PROBE_CAP &&
          tiles >= 1024;
 }
 
 // Enqueue the probe pass and the sort; returns the device tile order in *order.
+// quad: the Kerr-Schild probe on quads, -1 automatic, 0 never, 1 always (grt_debug_probe_keys).
 int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hipStream_t stream,
-                       const uint32_t** order) {
+                       const uint32_t** order, int quad_mode = -1) {
   const uint32_t tiles_x = wl.tiles_x, tiles_y = (uint32_t)(wl.n_items / 64 / wl.tiles_x);
   const uint64_t n = (uint64_t)tiles_x * tiles_y;
   size_t temp_bytes = 0;
@@ -546,7 +590,7 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   // Kerr-Schild probe rays on quads when they fill at most 2 waves per SIMD that way
   // (probe_quad_kernel: a C4 1/8 shard's 32,768 probes); above that the one-lane probe,
   // whose pass is then bound by its work, not by one probe's latency
-  const bool quad = g_probe_quad > 0 || (g_probe_quad < 0 && n <= (uint64_t)dc.cus * 128);
+  const bool quad = quad_mode > 0 || (quad_mode < 0 && n <= (uint64_t)dc.cus * 128);
   HIP_TRY(grt::launch_probe(s->desc.geometry, dc.d_scene, wl, (uint32_t)n, cap, probe, quad, stream));
   HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, cap, keys, keys_sorted, idx, ord, temp, &temp_bytes, stream));
   *order = ord;
@@ -558,12 +602,13 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
 // default the integrate kernel hands off once the queue is drained and no more rays are
 // live than the tail kernel integrates at once.  A lane holds at most one ray, so the
 // entry arena needs one entry per integrate lane whatever the threshold.
-int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, grt::TailList* tl, int* tail_blocks) {
+int tail_list(const grt_scene* s, DeviceCopy& dc, uint64_t lanes, long long tail, grt::TailList* tl,
+              int* tail_blocks) {
   std::memset(tl, 0, sizeof(*tl));
   *tail_blocks = 0;
-  if (s->desc.geometry != GRT_GEOM_KERR || g_tail == 0) return 0;
+  if (s->desc.geometry != GRT_GEOM_KERR || tail == 0) return 0;
   const int blocks = dc.cus * GRT_TAIL_WAVES;
-  const uint64_t threshold = g_tail > 0 ? (uint64_t)g_tail : (uint64_t)blocks * grt::TAIL_RAYS_PER_BLOCK;
+  const uint64_t threshold = tail > 0 ? (uint64_t)tail : (uint64_t)blocks * grt::TAIL_RAYS_PER_BLOCK;
   const uint64_t cap = lanes;
   if (cap > dc.tail_cap) {
     if (dc.tail_mem) {
@@ -617,17 +662,18 @@ int ray_times_reserve(uint64_t n, hipStream_t stream) {
 int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, const grt::Outputs& o,
                   unsigned long long* d_stats, hipStream_t stream) {
   grt::WorkList wl = wl_in;
+  const Knobs k = Knobs::now();
   if (int rc0 = stream_order(dc, stream)) return rc0;
-  if (schedule_wanted(s, wl)) {
+  if (schedule_wanted(s, wl, k)) {
     int rc0 = enqueue_tile_order(s, dc, wl, stream, &wl.tile_order);
     if (rc0) return rc0;
     // longest tiles to the priority wave of each SIMD, shortest to the others (WorkList)
-    wl.two_ended = (g_two_ended != 0 && wl.n_items < (1ull << 31)) ? 1u : 0u;
+    wl.two_ended = (k.two_ended != 0 && wl.n_items < (1ull << 31)) ? 1u : 0u;
   }
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
   if (dc.vol) HIP_TRY(hipMemsetAsync(dc.d_march, 0, 2 * sizeof(unsigned long long), stream));  // jobs, cursor
-  int threads = g_threads;
-  int blocks = g_blocks_per_cu > 0 ? dc.cus * g_blocks_per_cu
+  int threads = k.threads ? k.threads : 256;
+  int blocks = k.blocks_per_cu > 0 ? dc.cus * k.blocks_per_cu
                                    : dc.cus * 2 * grt::integrate_waves(s->desc.geometry, dc.vol);
   // never launch more lanes than there is work for
   uint64_t max_blocks = (wl.n_items + threads - 1) / threads;
@@ -656,7 +702,7 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
 #endif
   grt::TailList tl;
   int tail_blocks = 0;
-  rc = tail_list(s, dc, blocks * (uint64_t)threads, &tl, &tail_blocks);
+  rc = tail_list(s, dc, blocks * (uint64_t)threads, k.tail, &tl, &tail_blocks);
   if (rc) return rc;
   if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 16 * sizeof(unsigned long long), stream));
   HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
@@ -710,6 +756,13 @@ int validate_desc(const grt_scene_desc* d) {
 
 }  // namespace
 
+namespace grt_host {
+void scene_frame_size(const grt_scene* s, int64_t* rows, int64_t* cols) {
+  *rows = s->desc.camera.rows;
+  *cols = s->desc.camera.cols;
+}
+}  // namespace grt_host
+
 extern "C" {
 
 int grt_device_count(void) {
@@ -721,14 +774,13 @@ int grt_device_count(void) {
 int grt_set_launch_config(int blocks_per_cu, int threads_per_block) {
   if (blocks_per_cu < 0 || threads_per_block < 0 || threads_per_block % 64 != 0 || threads_per_block > 256)
     return fail(-EINVAL, "launch config: threads must be a multiple of 64 and <= 256");
-  g_blocks_per_cu = blocks_per_cu;
-  g_threads = threads_per_block ? threads_per_block : 256;
+  g_launch.store(((long long)blocks_per_cu << 16) | (threads_per_block ? threads_per_block : 256));
   return 0;
 }
 
 int grt_set_tail(long long threshold) {
   if (threshold < -1) return fail(-EINVAL, "tail threshold must be -1 (auto), 0 (off) or a ray count");
-  g_tail = threshold;
+  g_tail.store(threshold);
   return 0;
 }
 
@@ -741,9 +793,9 @@ int grt_tail_report(grt_scene* scene, int device, uint64_t* handed_off, double t
   if (!scene || !handed_off) return fail(-EINVAL, "null argument");
   *handed_off = 0;
   if (timeline_s) timeline_s[0] = timeline_s[1] = timeline_s[2] = 0.0;
-  if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
-    return 0;
-  DeviceCopy& dc = *scene->devices[device];
+  DeviceCopy* dcp = find_device(scene, device);
+  if (!dcp) return 0;
+  DeviceCopy& dc = *dcp;
   std::lock_guard<std::mutex> lock(dc.mu);
   HIP_TRY(hipSetDevice(device));
   unsigned long long v[16];
@@ -802,9 +854,9 @@ int grt_debug_ray_times_only(uint64_t k) {
 int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n, uint64_t* t0) {
   if (!scene || !out || !t0) return fail(-EINVAL, "null argument");
   if (n != g_rt_n || !g_rt) return fail(-EINVAL, "ray count differs from the last trace");
-  if (device < 0 || device >= (int)scene->devices.size() || !scene->devices[device] || !scene->devices[device]->ready)
-    return fail(-EINVAL, "no trace on this device");
-  DeviceCopy& dc = *scene->devices[device];
+  DeviceCopy* dcp = find_device(scene, device);
+  if (!dcp) return fail(-EINVAL, "no trace on this device");
+  DeviceCopy& dc = *dcp;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, g_rt, n * 6 * 8, hipMemcpyDeviceToHost));
@@ -830,11 +882,7 @@ int grt_debug_probe_keys(grt_scene* s, int device, const grt_row_shard* sh, int 
   wl.n_shards = sh->n_shards;
   if (wl.n_items / 64 != n_tiles || wl.n_items % 64 != 0) return fail(-EINVAL, "tile count differs");
   const uint32_t* order = nullptr;
-  const int saved = g_probe_quad;
-  g_probe_quad = quad;
-  rc = enqueue_tile_order(s, *dc, wl, nullptr, &order);
-  g_probe_quad = saved;
-  if (rc) return rc;
+  if ((rc = enqueue_tile_order(s, *dc, wl, nullptr, &order, quad))) return rc;
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(keys_out, dc->sched_mem, n_tiles * 4, hipMemcpyDeviceToHost));
   return 0;
@@ -903,19 +951,19 @@ int grt_debug_path_counts(uint64_t* out, int reset) {
 // (DevScene::div_fast = 0), so a test can hold the range-free forms to them end to end.
 int grt_debug_range_free(int on) {
   if (on != 0 && on != 1) return fail(-EINVAL, "range-free arithmetic: 0 or 1");
-  g_range_free = on;
+  g_range_free.store(on);
   return 0;
 }
 
 int grt_set_two_ended(int on) {
   if (on != 0 && on != 1) return fail(-EINVAL, "two-ended queue: 0 or 1");
-  g_two_ended = on;
+  g_two_ended.store(on);
   return 0;
 }
 
 int grt_set_schedule(int mode) {
   if (mode < -1 || mode > 1) return fail(-EINVAL, "schedule mode must be -1 (auto), 0 or 1");
-  g_schedule = mode;
+  g_schedule.store(mode);
   return 0;
 }
 
@@ -953,8 +1001,8 @@ int grt_scene_create(const grt_scene_desc* desc, grt_scene** out) {
 
 int grt_scene_destroy(grt_scene* s) {
   if (!s) return 0;
-  for (size_t dev = 0; dev < s->devices.size(); ++dev) {
-    DeviceCopy* dc = s->devices[dev];
+  for (int dev = 0; dev < grt_scene::MAX_DEVICES; ++dev) {
+    DeviceCopy* dc = s->devices[dev].load(std::memory_order_acquire);
     if (!dc) continue;
     (void)hipSetDevice((int)dev);
     for (void* p : dc->allocations) (void)hipFree(p);
@@ -1338,7 +1386,7 @@ static int ad_reserve(DeviceCopy& dc, uint64_t bytes) {
 }
 
 constexpr uint64_t SUB_CHUNK = 1ull << 21;  // sub-rays per supersample trace launch
-uint64_t g_sub_chunk = SUB_CHUNK;            // grt_set_sub_chunk (tests force several chunks)
+std::atomic<uint64_t> g_sub_chunk{SUB_CHUNK};  // grt_set_sub_chunk (tests force several chunks)
 
 // Buffers of the supersample pass over at most n_max selected pixels.
 struct SuperBufs {
@@ -1350,9 +1398,11 @@ struct SuperBufs {
   uint8_t *cls = nullptr, *status = nullptr, *stop = nullptr;
   uint32_t* steps = nullptr;
   unsigned long long* live = nullptr;
-  void carve(AdArena& A, uint64_t n_max, uint32_t spa) {
+  // sub_chunk: grt_set_sub_chunk's value, read once per call (the plan and the carve of
+  // one call must agree)
+  void carve(AdArena& A, uint64_t n_max, uint32_t spa, uint64_t sub_chunk) {
     per = spa * spa;
-    chunk_pix = std::max<uint64_t>(1, std::min<uint64_t>(n_max, g_sub_chunk / per));
+    chunk_pix = std::max<uint64_t>(1, std::min<uint64_t>(n_max, sub_chunk / per));
     n_chunks = (uint32_t)((n_max + chunk_pix - 1) / chunk_pix);
     cap = chunk_pix * per;
     pix = (uint32_t*)A.take(cap * 4);
@@ -1507,6 +1557,7 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
   const bool device_floor = supersampled && !cfg->has_minimum_luminance;
   if (supersampled && n > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "section larger than INT_MAX pixels");
   const uint32_t spa = cfg->samples_per_axis;
+  const uint64_t sub_chunk = g_sub_chunk.load(std::memory_order_relaxed);
   // plan: section buffers, selection, floor, sort / compaction scratch, sub-ray buffers
   size_t sort_bytes = 0, select_bytes = 0;
   if (device_floor) HIP_TRY(grt::luminance_floor_device(nullptr, 4, n, floor_index(n), nullptr, &sort_bytes, nullptr, 0));
@@ -1532,7 +1583,7 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
     *floor = (double*)A.take(8);
     *sort = A.take(sort_bytes);
     *select = A.take(select_bytes);
-    if (!mask_xyza) B->carve(A, n, spa);
+    if (!mask_xyza) B->carve(A, n, spa, sub_chunk);
     fails.key = (uint64_t*)A.take(fail_cap * 8);
     fails.status = (uint8_t*)A.take(fail_cap);
     if (want_events) {  // NaN / no-terminal-event sub-rays too (scene.rs:178-183, :196-202)
@@ -1687,13 +1738,13 @@ int grt_render_shard(grt_scene* s, int device, const grt_row_shard* sh, float* x
 
 int grt_set_sub_chunk(uint64_t sub_rays) {
   if (sub_rays > (1ull << 31)) return fail(-EINVAL, "sub-ray chunk larger than 2^31");
-  g_sub_chunk = sub_rays ? sub_rays : SUB_CHUNK;
+  g_sub_chunk.store(sub_rays ? sub_rays : SUB_CHUNK);
   return 0;
 }
 
 int grt_set_hit_pool_min(uint64_t records) {
   if (records == 0 || records > POOL_MAX) return fail(-EINVAL, "hit pool minimum must be in [1, 2^31)");
-  g_pool_min = records;
+  g_pool_min.store(records);
   return 0;
 }
 
@@ -1757,6 +1808,7 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
   }
   if (n_local > (uint64_t)INT_MAX) return fail(-EOVERFLOW, "shard larger than INT_MAX pixels");
   const uint32_t spa = cfg->samples_per_axis;
+  const uint64_t sub_chunk = g_sub_chunk.load(std::memory_order_relaxed);
   const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
   const bool want_events = fail_cap && failures->stop;
   size_t select_bytes = 0;
@@ -1773,7 +1825,7 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
     sel_frame = (uint32_t*)A.take(n_local * 4);
     d_cnt = (unsigned long long*)A.take(16);  // [0] selected pixels, [1] failed sub-samples
     b_select = A.take(select_bytes);
-    if (!sampling_mask_xyza) B.carve(A, n_local, spa);
+    if (!sampling_mask_xyza) B.carve(A, n_local, spa, sub_chunk);
     fails.key = (uint64_t*)A.take(fail_cap * 8);
     fails.status = (uint8_t*)A.take(fail_cap);
     if (want_events) {  // NaN / no-terminal-event sub-rays too (scene.rs:178-183, :196-202)

@@ -70,9 +70,6 @@ namespace grt {
 #ifndef GRT_KL_STAGES
 #define GRT_KL_STAGES 4  // how many leading stages (k1, k2, ...) those kernels park in LDS
 #endif
-#ifndef GRT_CLAIM_REFRESH
-#define GRT_CLAIM_REFRESH 0  // experiment: KerrBL reads the work counter before a chunk claim
-#endif
 #ifndef GRT_TAIL_PRIO
 #define GRT_TAIL_PRIO 1  // light charts: issue priority by steps left once the queue drains (C5 -1.2%, profiles/r05i)
 #endif
@@ -2087,18 +2084,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
       // worth of lanes of the end: its 2.25M short rays end ~13M times a second, and an
       // atomic on one address per refill cost C3 +16% (profiles/r05l, r05m).
       const uint64_t grid_lanes = (uint64_t)gridDim.x * blockDim.x;
-      bool exact = TAIL || two_ended || G != GRT_GEOM_KERR_BL || chunk_end + 2 * grid_lanes >= n_items;
-#if GRT_CLAIM_REFRESH
-      if (!exact && cnt > remaining) {
-        // the wave's view (its last chunk's end) is old when its lanes ran slowly: before a
-        // chunk claim, read the counter, so that a wave the arbiter served last does not
-        // take 64 items near the end of the queue and start them one ray lifetime late
-        unsigned long long c0 = 0;
-        if (lane == 0) c0 = load_agent(counter);
-        c0 = __shfl(c0, 0);
-        exact = c0 + 2 * grid_lanes >= n_items;
-      }
-#endif
+      const bool exact = TAIL || two_ended || G != GRT_GEOM_KERR_BL || chunk_end + 2 * grid_lanes >= n_items;
       const uint64_t take = exact ? cnt - remaining : CHUNK;
       if (cnt > remaining) {
         unsigned long long b = 0;
@@ -2167,14 +2153,9 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
         }
       }
       w_rays += __popcll(__ballot(fresh));
-#ifndef GRT_TAIL_PRIO_BL
-#define GRT_TAIL_PRIO_BL 0  // experiment: the same for KerrBL, with len = GRT_TAIL_PRIO_BL_LEN accepted steps
-#endif
-#ifndef GRT_TAIL_PRIO_BL_LEN
-#define GRT_TAIL_PRIO_BL_LEN 1200.0
-#endif
 #if GRT_TAIL_PRIO
-      if constexpr (!TAIL && (G != GRT_GEOM_KERR_BL || GRT_TAIL_PRIO_BL)) {  // KerrBL's rays are all short
+      // KerrBL's rays are all short: measured no gain there
+      if constexpr (!TAIL && G != GRT_GEOM_KERR_BL) {
         // After the queue has drained for this wave (one of its lanes found no item), the
         // pass ends on the rays with the most steps left, so the waves holding them get the
         // SIMD's issue slots first (s_setprio; the arbiter otherwise serves the oldest wave):
@@ -2184,7 +2165,7 @@ __global__ void __launch_bounds__(256, integrate_waves(G, VOL)) integrate_kernel
           uint32_t mi = active ? (uint32_t)i : 0xffffffffu;
 #pragma unroll
           for (int off = 32; off > 0; off >>= 1) mi = min(mi, (uint32_t)__shfl_xor((int)mi, off));
-          const double len = G == GRT_GEOM_KERR_BL ? GRT_TAIL_PRIO_BL_LEN : sqrt(S.max_radius_sq);
+          const double len = sqrt(S.max_radius_sq);
           const double left = len - (double)mi;
           if (left > 0.67 * len) __builtin_amdgcn_s_setprio(3);
           else if (left > 0.33 * len) __builtin_amdgcn_s_setprio(2);
@@ -2794,6 +2775,18 @@ GDEV bool probe_escaped(const DevScene& S, const double* y, double& r_prev, uint
   }
 }
 
+// The probe's radial coordinate at its initial state, so that the first accepted step's
+// "moving outward" test compares against where the ray started (a camera far from the
+// hole, beyond the escape radius, must not end its inward probes at step 1).
+template <int G>
+GDEV double probe_r0(const DevScene& S, const double* y) {
+  if constexpr (G != GRT_GEOM_KERR || !GRT_PROBE_ESCAPE) {
+    return 0.0;
+  } else {
+    return sqrt(ks_r_sqr(S.a, y[1], y[2], y[3]));
+  }
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ Sp, WorkList wl, uint32_t n_tiles,
                                                    uint32_t cap, uint32_t* __restrict__ steps_out) {
@@ -2810,7 +2803,7 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
   const uint64_t end = S.max_steps < (uint64_t)cap ? S.max_steps : (uint64_t)cap;
   uint64_t i = 1;
   double h = S.step_size;
-  double r_prev = 0.0;
+  double r_prev = probe_r0<G>(S, y);
   uint32_t key = 0;
   bool escaped = false;
   for (; i < end; ++i) {
@@ -2866,7 +2859,7 @@ __global__ void __launch_bounds__(256, 2) probe_quad_kernel(const DevScene* __re
   const uint64_t end = S.max_steps < (uint64_t)cap ? S.max_steps : (uint64_t)cap;
   uint64_t i = 1;
   double h = S.step_size;
-  double r_prev = 0.0;
+  double r_prev = probe_r0<G>(S, y);
   uint32_t key = 0;
   bool escaped = false;
   for (; i < end; ++i) {  // identical decisions in the quad's four lanes

@@ -12,6 +12,8 @@
 namespace grt_host {
 
 void set_error(const std::string& msg);
+// The camera frame of a device scene (grt_scene_desc.camera rows x cols; api.hip).
+void scene_frame_size(const grt_scene* s, int64_t* rows, int64_t* cols);
 double rclamp_pub(double v, double lo, double hi);
 int camera_build(int geometry, double radius, double a, const double position[4], const double velocity[4],
                  double alpha, int64_t rows, int64_t cols, double phi, double theta, double psi,

@@ -25,10 +25,11 @@ import time
 RENDER_FLAGS = ("--filename", "--from-row", "--from-col", "--to-row", "--to-col")
 
 
-# Debug names of the RaytracerError variants a pixel can end in (grt_main.cpp's table)
 # exit status of a frame written with pixels that lost hit candidates (the device hit pool
 # could not hold them after two reserves): the image is incomplete
 EXIT_INCOMPLETE = 3
+
+# Debug names of the RaytracerError variants a pixel can end in (grt_main.cpp's table)
 ERROR_NAMES = {1: "IntegrationError(MaxStepsReached)", 2: "NoCircularOrbitPossible", 3: "BelowRISCO",
                4: "NonFiniteRadius"}
 
@@ -104,6 +105,35 @@ def parse_args(argv):
     return a
 
 
+def trace_until_complete(render_once, lost_pixels, grow_pool, log, attempts: int = 3):
+    """Trace the frame until no pixel lost hit candidates, at most `attempts` times.
+
+    render_once() traces the frame and returns its result; lost_pixels() returns the
+    number of pixels that lost candidates in that trace, summed over every rank (the same
+    value on each rank, so every rank takes the same branch); grow_pool() grows this
+    rank's device hit pool from the trace's measured need (grt_hit_pool_reserve).
+    Returns (result of the last trace, pixels still incomplete after it: 0 or the count)."""
+    out = None
+    for attempt in range(attempts):
+        out = render_once()
+        lost = lost_pixels()
+        if lost == 0:
+            return out, 0
+        if attempt == attempts - 1:  # the pool cannot hold them (2^31 records): the frame is incomplete
+            log(f"ERROR {lost} pixels lost hit candidates after growing the device hit pool {attempts - 1} "
+                f"times; they are written without their candidates past the first 16, and the exit status "
+                f"is {EXIT_INCOMPLETE}")
+            return out, lost
+        log(f"WARN {lost} pixels lost hit candidates (device hit pool full); growing the pool and tracing again")
+        grow_pool()
+    return out, 0
+
+
+def exit_status(incomplete: int) -> int:
+    """Process exit status of a rank: EXIT_INCOMPLETE when the written frame lacks candidates."""
+    return EXIT_INCOMPLETE if incomplete else 0
+
+
 def main(argv=None) -> int:
     a = parse_args(sys.argv[1:] if argv is None else argv)
     t_start = time.perf_counter()
@@ -166,33 +196,35 @@ def main(argv=None) -> int:
         supersampled = bool(cfg.enabled) or mask is not None
         if supersampled and rank == 0:  # raytracer.rs:264-267
             _log(f"[render_dist] INFO Rendering section from (0, 0) to ({scene.rows}, {scene.cols}) with supersampling")
-        incomplete = 0  # pixels still missing hit candidates after the last trace
-        for attempt in range(3):
+        fails = None
+        report = {}
+
+        def render_once():
+            nonlocal fails, report
             fails = L.SubsampleFailures(fail_cap, L.ptr(f_pix, C.c_uint32), L.ptr(f_smp, C.c_uint32),
                                         L.ptr(f_st, C.c_uint8), 0, L.ptr(f_stop, C.c_uint8), L.ptr(f_steps, C.c_uint32))
             report = {}
             stats.zero_()
-            out = render_frame_adaptive(scene, rank, world, band_rows=a.band_rows, device=device, stats=stats,
+            res = render_frame_adaptive(scene, rank, world, band_rows=a.band_rows, device=device, stats=stats,
                                         sampling_mask_xyza=mask, tone_mapping=None if want_f64 else tone,
                                         failures=C.byref(fails), report=report)
             torch.cuda.synchronize()
-            # a device hit pool too small for some ray's candidates (grt_hit_pool_reserve):
-            # every rank grows its pool and the frame is traced again, complete
+            return res
+
+        def lost_pixels():
+            # a device hit pool too small for some ray's candidates: every rank sees the sum
             lost = stats[3:4].clone() if dist.get_backend() != "gloo" else stats[3:4].cpu()
             dist.all_reduce(lost)
-            if int(lost[0]) == 0:
-                break
-            if attempt == 2:  # the pool cannot hold them (2^31 records): the frame is incomplete
-                incomplete = int(lost[0])
-                if rank == 0:
-                    _log(f"[render_dist] ERROR {incomplete} pixels lost hit candidates after growing the device "
-                          "hit pool twice; they are written without their candidates past the first "
-                          f"{L.GRT_MAX_HITS}, and the exit status is {EXIT_INCOMPLETE}")
-                break
+            return int(lost[0])
+
+        def log_rank0(msg):
             if rank == 0:
-                _log(f"[render_dist] WARN {int(lost[0])} pixels lost hit candidates (device hit pool full); "
-                      "growing the pool and tracing again")
-            L.check(L.lib().grt_hit_pool_reserve(scene._s, device, 0, None), "grt_hit_pool_reserve")
+                _log(f"[render_dist] {msg}")
+
+        out, incomplete = trace_until_complete(
+            render_once, lost_pixels,
+            lambda: L.check(L.lib().grt_hit_pool_reserve(scene._s, device, 0, None), "grt_hit_pool_reserve"),
+            log_rank0)
         t_render = time.perf_counter() - t0
         # each rank logs its own pixels, in pixel order (the reference logs from its parallel loop):
         # raytracer.rs:232-239 the failed pixels; scene.rs:178-183 / :196-202 the error-free rays that
@@ -227,7 +259,7 @@ def main(argv=None) -> int:
             dist.all_reduce(stats)
             totals = stats.cpu()
         if rank != 0:
-            return EXIT_INCOMPLETE if incomplete else 0
+            return exit_status(incomplete)
         w, h = scene.cols, scene.rows
         if want_f64:
             xyza64, _cls, _status, n_sel = out
@@ -251,7 +283,7 @@ def main(argv=None) -> int:
               f"{n_sel} supersampled pixels, frame {t_render:.3f} s ({steps / t_render:.3e} steps/s)")
         _log(f"[render_dist] INFO saved image to {a.filename}")  # raytracer.rs:494, main.rs:175-176
         _log(f"[render_dist] INFO Elapsed time: {duration_debug_2(time.perf_counter() - t_start)}")
-        return EXIT_INCOMPLETE if incomplete else 0
+        return exit_status(incomplete)
     finally:
         dist.destroy_process_group()
 

@@ -233,6 +233,66 @@ class Scene:
         res.stats = _stats_dict(st)
         return res
 
+    def render_frame_multi(self, devices=(0,), band_rows: int = 16, adaptive: Optional[L.AdaptiveConfig] = None,
+                           supersample: bool = False, sampling_mask_xyza=None, fields=("xyza", "class", "status"),
+                           fail_capacity: int = 0) -> dict:
+        """The whole frame over `devices` (grt_render_frame_multi: cyclic row bands, one host
+        thread per device, one RCCL gather to devices[0]).  fields: which of "xyza" (f32),
+        "xyza64", "class", "status", "stop", "steps" to return (frame order).  supersample:
+        the adaptive pass with `adaptive` (default: the scene's own configuration).
+        Returns a dict of the fields plus "stats", "n_supersampled", "report" and, with
+        fail_capacity, "failures" (pixel, sample, status, stop, steps arrays)."""
+        n = self.rows * self.cols
+        want = set(fields)
+        arrays = {}
+        if "xyza" in want:
+            arrays["xyza"] = np.zeros((n, 4), np.float32)
+        if "xyza64" in want or supersample or sampling_mask_xyza is not None:
+            arrays["xyza64"] = np.zeros((n, 4), np.float64)
+        for k, dt in (("class", np.uint8), ("status", np.uint8), ("stop", np.uint8), ("steps", np.uint32)):
+            if k in want:
+                arrays[k] = np.zeros(n, dt)
+        out = L.FrameOut(L.ptr(arrays["xyza"], C.c_float) if "xyza" in arrays else None,
+                         L.dptr(arrays["xyza64"]) if "xyza64" in arrays else None,
+                         L.ptr(arrays["class"], C.c_uint8) if "class" in arrays else None,
+                         L.ptr(arrays["status"], C.c_uint8) if "status" in arrays else None,
+                         L.ptr(arrays["stop"], C.c_uint8) if "stop" in arrays else None,
+                         L.ptr(arrays["steps"], C.c_uint32) if "steps" in arrays else None)
+        cfg = None
+        if supersample or sampling_mask_xyza is not None:
+            cfg = L.AdaptiveConfig()
+            C.memmove(C.byref(cfg), C.byref(adaptive if adaptive is not None else self.adaptive), C.sizeof(cfg))
+            cfg.enabled = 1 if supersample else cfg.enabled
+        mask = None
+        if sampling_mask_xyza is not None:
+            mask = np.ascontiguousarray(sampling_mask_xyza, np.float64)
+        devs = (C.c_int * len(devices))(*devices)
+        fails = None
+        farr = {}
+        if fail_capacity:
+            farr = {"pixel": np.zeros(fail_capacity, np.uint32), "sample": np.zeros(fail_capacity, np.uint32),
+                    "status": np.zeros(fail_capacity, np.uint8), "stop": np.zeros(fail_capacity, np.uint8),
+                    "steps": np.zeros(fail_capacity, np.uint32)}
+            fails = L.SubsampleFailures(fail_capacity, L.ptr(farr["pixel"], C.c_uint32),
+                                        L.ptr(farr["sample"], C.c_uint32), L.ptr(farr["status"], C.c_uint8), 0,
+                                        L.ptr(farr["stop"], C.c_uint8), L.ptr(farr["steps"], C.c_uint32))
+        nsel = C.c_uint64(0)
+        st = L.Stats()
+        rep = L.MultiReport()
+        L.check(L.lib().grt_render_frame_multi(self._s, len(devices), devs, band_rows,
+                                               C.byref(cfg) if cfg is not None else None,
+                                               L.dptr(mask) if mask is not None else None, C.byref(out),
+                                               C.byref(nsel), C.byref(st), C.byref(fails) if fails is not None else None,
+                                               C.byref(rep)), "grt_render_frame_multi")
+        arrays["stats"] = _stats_dict(st)
+        arrays["n_supersampled"] = int(nsel.value)
+        arrays["report"] = rep
+        if fails is not None:
+            m = min(int(fails.count), fail_capacity)
+            arrays["failures"] = {k: v[:m] for k, v in farr.items()}
+            arrays["failures"]["count"] = int(fails.count)
+        return arrays
+
     def render_section(self, from_row: int = 0, from_col: int = 0, to_row: Optional[int] = None,
                        to_col: Optional[int] = None, adaptive: Optional[L.AdaptiveConfig] = None,
                        sampling_mask_xyza=None, device: int = 0):

@@ -442,6 +442,65 @@ int grt_render_shard_async(grt_scene* scene, int device, void* stream, const grt
                            float* d_xyza, uint8_t* d_class, uint8_t* d_status, double* d_xyza64,
                            uint32_t* d_steps, uint8_t* d_stop, uint64_t* d_stats);
 
+/* ---- one frame across several GPUs of this process (north_star) ----
+ * The north-star layout behind the C ABI: the frame's rows in cyclic bands of band_rows
+ * (band b -> devices[b % n_devices], grt_row_shard), one host thread per device tracing
+ * its bands (grt_render_shard_async), and ONE RCCL gather (grouped send / receive over
+ * xGMI, one communicator per device from ncclCommInitAll) of every device's pixel records
+ * to devices[0], where a kernel de-interleaves them into frame order.  With supersampling
+ * (cfg->enabled, or a sampling mask) one RCCL allgather of each pixel's (Y, alpha, class)
+ * (17 B) comes first: the selection stencil reads neighbours in other devices' bands and
+ * the luminance floor is a percentile of the whole frame; each device then supersamples
+ * its own pixels (grt_supersample_shard_device).  Replaces the single-process frame
+ * driver of the `render` command: render_section_to_cie_buffer[_raw|_supersampled]
+ * (raytracer.rs:195-318) as Raytracer::render_section calls it (:460-497, main.rs:80-116).
+ * Every pixel equals grt_render_pixels / grt_render_section_ex of the same frame on one
+ * device.  The communicators, streams and device scratch are created on the first call
+ * for a device list and kept (grt_multi_release frees them). */
+#define GRT_MULTI_MAX_DEVICES 16
+
+/* Host outputs in frame order (camera rows x cols); a NULL field is not gathered.  The
+ * gather moves 2 B per pixel (class, status) plus the requested fields: f32 XYZA + class
+ * + status is the 18-B pixel record of the 1-spp frame. */
+typedef struct grt_frame_out {
+  float* xyza;         /* f32 XYZA (1-spp frames only: NULL with supersampling)          */
+  double* xyza64;      /* f64 XYZA, the supersampled colour where selected (required with
+                          supersampling)                                                  */
+  uint8_t* ray_class;  /* RayClass of the 1-spp ray                                       */
+  uint8_t* status;     /* grt_status of the 1-spp ray (raytracer.rs:232-239)              */
+  uint8_t* stop;       /* grt_stop_reason of the 1-spp ray                                */
+  uint32_t* steps;     /* accepted steps of the 1-spp ray                                 */
+} grt_frame_out;
+
+typedef struct grt_multi_report {
+  uint32_t n_devices;
+  uint32_t record_bytes;     /* bytes per pixel the gather moved                                */
+  uint32_t attempts;         /* traces of the frame (more than 1 when a hit pool had to grow)   */
+  uint32_t _pad;
+  double wall_ms;            /* the whole call, host clock                                      */
+  double gather_ms;          /* last trace: RCCL gather + de-interleave on devices[0] (events)  */
+  double allgather_ms;       /* supersampling: the (Y, alpha, class) allgather, max over devices */
+  double trace_ms[GRT_MULTI_MAX_DEVICES];        /* per device: its trace (+ supersample pass)   */
+  uint64_t accepted_steps[GRT_MULTI_MAX_DEVICES];
+  uint64_t rows[GRT_MULTI_MAX_DEVICES];          /* frame rows each device traced                */
+} grt_multi_report;
+
+/* Render the whole camera frame over n_devices distinct GPUs (1 <= n <= 16; n = 1 runs the
+ * same RCCL path with a one-rank communicator).  cfg (nullable): the scene's adaptive
+ * configuration (grt_host_scene_adaptive), NULL or !enabled = 1 spp; sampling_mask_xyza
+ * (nullable): paint the selected pixels instead (--show-sampling-mask).  stats: summed
+ * counters, kernel_ms the slowest device's trace.  failures (nullable): every device's
+ * failed sub-samples, frame pixel indices, sorted by (pixel, sample).  A trace that lost
+ * hit candidates grows the pools and traces the frame again (at most 3 traces; after
+ * that the pixels keep GRT_FLAG_HIT_OVERFLOW and stats->hit_overflows counts them). */
+int grt_render_frame_multi(grt_scene* scene, int n_devices, const int* devices, uint32_t band_rows,
+                           const grt_adaptive_config* cfg, const double* sampling_mask_xyza,
+                           const grt_frame_out* out, uint64_t* n_supersampled, grt_stats* stats,
+                           grt_subsample_failures* failures, grt_multi_report* report);
+/* Free the communicators, streams and scratch grt_render_frame_multi keeps (no frame may
+ * be in flight). */
+void grt_multi_release(void);
+
 /* The device hit pool that keeps the window candidates past a ray's GRT_MAX_HITS slots
  * (no reference counterpart: the reference's per-ray Vec grows, scene.rs:139-152).
  * A trace starts with the pool at its minimum (grt_set_hit_pool_min, 2^20 records) or

@@ -36,7 +36,8 @@ def test_struct_layout_matches_header(grt, tmp_path):
                "grt_object_desc": L.ObjectDesc, "grt_global_opts": L.GlobalOpts,
                "grt_adaptive_config": L.AdaptiveConfig, "grt_stats": L.Stats, "grt_offsets": L.Offsets,
                "grt_aux_out": L.AuxOut, "grt_row_shard": L.RowShard,
-               "grt_subsample_failures": L.SubsampleFailures}
+               "grt_subsample_failures": L.SubsampleFailures, "grt_frame_out": L.FrameOut,
+               "grt_multi_report": L.MultiReport}
     src = tmp_path / "sizes.c"
     body = "".join(f'  printf("{k} %zu\\n", sizeof({k}));\n' for k in structs)
     src.write_text(f'#include <stdio.h>\n#include "grt_api.h"\nint main(void) {{\n{body}  return 0;\n}}\n')

@@ -231,3 +231,15 @@ def test_c2_frame_loop_gloo_world2():
         assert got[r]["elapsed"] > 0.0
     # slot 0's last frame is number 6 (timed k = 4), slot 1's number 5 (k = 3), from each rank
     assert got[0]["gathered"] == [[6.0, 106.0], [5.0, 105.0]]
+
+
+def test_parse_cli_phases():
+    import bench
+
+    err = ("[grt] INFO Using coordinate system: Spherical\n[grt] 2250000 rays, 34000000000 accepted steps, "
+           "34012345678 attempts, 0 supersampled pixels, kernel 1287.0 ms (2.6e10 steps/s)\n"
+           "[grt] INFO saved image to x.png\n[grt] phases (ms): load 210.5, create 0.1, render 1601.2, output 3.4, "
+           "write 95.0, since start 1950.3\n[grt] INFO Elapsed time: 1.95s\n")
+    p = bench.parse_cli_phases(err)
+    assert p["load_ms"] == 210.5 and p["render_ms"] == 1601.2 and p["since_start_ms"] == 1950.3
+    assert p["elapsed_line"] == "1.95s" and p["rays"] == 2250000 and p["accepted_steps"] == 34000000000

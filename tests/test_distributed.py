@@ -97,3 +97,59 @@ def test_shard_rows_partition_the_frame_and_match_the_c_abi(grt):
     # invalid shards have no rows
     assert lib.grt_shard_row_count(100, C.byref(L.RowShard(8, 2, 2))) == 0
     assert lib.grt_shard_row_count(100, C.byref(L.RowShard(0, 0, 2))) == 0
+
+
+def _incomplete_worker(rank, world, port, out_dir, lost_per_rank):
+    import sys
+
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+
+    from gr_raytracer_amd.render_dist import EXIT_INCOMPLETE, exit_status, trace_until_complete
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = {"render": 0, "grow": 0}
+        logs = []
+
+        def render_once():
+            calls["render"] += 1
+            return f"frame {calls['render']}"
+
+        def lost_pixels():  # only this rank's pixels lose candidates, on every trace
+            t = torch.tensor([lost_per_rank[rank]], dtype=torch.int64)
+            dist.all_reduce(t)
+            return int(t[0])
+
+        def grow():
+            calls["grow"] += 1
+
+        out, incomplete = trace_until_complete(render_once, lost_pixels, grow, logs.append)
+        status = exit_status(incomplete)
+        assert EXIT_INCOMPLETE == 3
+        with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
+            f.write(f"{out}|{incomplete}|{status}|{calls['render']}|{calls['grow']}|{len(logs)}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("lost_per_rank,expect", [((0, 4), (3, 4, 3)), ((0, 0), (1, 0, 0))])
+def test_render_dist_incomplete_frame_exit_status_gloo(lost_per_rank, expect):
+    """render_dist's hit-pool retry loop (trace_until_complete) over gloo, world 2: when one
+    rank's pixels lose candidates on all three traces, EVERY rank gets the all-reduced
+    count and exits with EXIT_INCOMPLETE (3) after growing its pool twice; with nothing
+    lost each rank traces once and exits 0."""
+    import torch.multiprocessing as mp
+
+    renders, incomplete, status = expect
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_incomplete_worker, args=(2, _free_port(), d, lost_per_rank), nprocs=2, join=True)
+        for r in range(2):
+            out, inc, st, n_render, n_grow, n_logs = open(os.path.join(d, f"rank{r}.txt")).read().split("|")
+            assert out == f"frame {renders}"
+            assert int(inc) == incomplete and int(st) == status
+            assert int(n_render) == renders and int(n_grow) == max(0, renders - 1)
+            assert int(n_logs) == (renders if incomplete else 0)

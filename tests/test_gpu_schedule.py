@@ -38,3 +38,51 @@ def test_probe_keys_on_quads_equal_one_lane_keys(grt, gpu, size, shard):
     assert (keys[0] > 0).all()
     assert (keys[0] >= cap).any() and (keys[0] < cap).any()  # capped probes and finished ones
     assert (keys[0] == cap - 1).any()  # probes that ended outward-bound (probe_escaped)
+
+
+def _probe_keys(grt, toml, opts, shard, quad):
+    from conftest import host_scene as hsc
+    from gr_raytracer_amd import _lib as L
+
+    hs = hsc(grt, toml, opts)
+    scene = grt.Scene(hs.desc_ptr(), keepalive=hs)
+    lib = L.lib()
+    sh = L.RowShard(16, *shard)
+    rows = lib.grt_shard_row_count(opts.height, C.byref(sh))
+    n_tiles = ((rows + 7) // 8) * ((opts.width + 7) // 8)
+    fn = lib.grt_debug_probe_keys
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_void_p, C.c_int, C.POINTER(L.RowShard), C.c_int, C.c_void_p, C.c_uint64]
+    k = np.zeros(n_tiles, np.uint32)
+    L.check(fn(scene._s, 0, C.byref(sh), quad, k.ctypes.data, n_tiles), "grt_debug_probe_keys")
+    return k
+
+
+def test_probe_keys_far_kerr_camera_keep_inward_probes(grt, gpu):
+    """A Kerr-Schild camera far beyond the escape radius (r = 30 > 10 radius): a probe is
+    'outward-bound' only once its r grows past where it started, so the inward probes
+    run on and the horizon creepers reach the cap (keys >= cap).  With the probe's
+    previous radius starting at 0, every probe ended at step 1 with the key cap - 1."""
+    opts = grt.GlobalOpts(width=256, height=256, camera_position=(-30.0, 0.0, -0.5), theta=1.52, psi=-1.57,
+                          phi=0.0, max_steps=1000000)
+    cap = int(min(32768, max(4096, 0.3 * 15000)))
+    keys = {q: _probe_keys(grt, "kerr.toml", opts, (0, 1), q) for q in (0, 1)}
+    assert np.array_equal(keys[0], keys[1])
+    k = keys[0]
+    assert (k == cap - 1).any()  # escaping probes still end early
+    assert (k >= cap).sum() >= 8  # the shadow's tiles: capped probes, keyed by their horizon distance
+    assert not (k == cap - 1).all()
+
+
+def test_probe_keys_schwarzschild_escaping_probes_finish_below_the_cap(grt, gpu):
+    """Schwarzschild has no outward-bound shortcut, so its probe cap stays 1.3 x max_radius
+    (api.hip probe_cap): an escaping probe (~max_radius unit steps) finishes below the cap
+    and is keyed by its own length, under every capped probe, instead of being capped at
+    0.3 x max_radius and keyed by its distance to the horizon ahead of the long rays."""
+    opts = grt.GlobalOpts(width=256, height=256, camera_position=(-16.0, 0.0, 3.5), theta=-3.142, psi=0.0, phi=0.0,
+                          max_steps=1000000)
+    cap = int(min(32768, max(4096, 1.3 * 15000)))
+    k = _probe_keys(grt, "schwarzschild.toml", opts, (0, 1), 0)
+    escaping = (k > 0.3 * 15000) & (k < cap)
+    assert escaping.sum() > len(k) // 2  # most of the frame sees the celestial sphere
+    assert np.median(k[escaping]) > 0.6 * 15000  # they ran out to max_radius, uncapped
