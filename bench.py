@@ -448,6 +448,29 @@ def run_c2(args, rank, world, local_rank, dev):
         line["roofline"]["single_launch_basis"] = (
             f"{len(single_ms)} frames rendered alone after the timed region (one in flight, slot 0's stream), "
             f"shortest launch; HIP events around grt_render_pixels_async (integrate + shade kernels)")
+    if world == 1 and args.fused_check and args.arith == "exact":
+        # the same loop in the fused arithmetic mode (grt_set_arithmetic(1): FMA contraction in
+        # the light charts' kernels, pixels within 1e-4 of the reference on every robust pixel,
+        # tests/test_fused.py), measured beside the exact headline
+        g.set_arithmetic("fused")
+        try:
+            evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.steps)]
+            el_f = c2_frame_loop(F, args.steps, 1, render, None, lambda: torch.cuda.synchronize(dev),
+                                 lambda: None, reset, lambda k, e, j: evf[k][e].record(slots[j]["stream"]))
+            kms_f = (sum(a.elapsed_time(b) for a, b in evf) / args.steps if F == 1 else
+                     max(evf[0][0].elapsed_time(e[1]) for e in evf[-F:]) / args.steps)
+            cf = [sum(v) for v in zip(*(s["stats"].cpu().tolist() for s in slots))]
+        finally:
+            g.set_arithmetic("exact")
+        rf = roofline("c2", "schwarzschild", cf[0] / args.steps, cf[1] / args.steps, kms_f, n, "")
+        line["fused"] = {"value": cf[0] / el_f, "ms_per_step": el_f / args.steps * 1e3, "kernel_ms": kms_f,
+                         "frac": rf["frac"], "accepted_steps_per_frame": cf[0] / args.steps,
+                         "speedup_vs_exact": (elapsed / args.steps) / (el_f / args.steps),
+                         "mode": "grt_set_arithmetic(1): the light charts' kernels with FMA contraction "
+                                 "(geodesic_fused.hip); same loop, frames and slots as the headline; parity bar "
+                                 "1e-4 relative per channel on every robust pixel (tests/test_fused.py), not bit "
+                                 "identity"}
     if world == 1 and not args.no_cli_wall:
         torch.cuda.synchronize(dev)
         line["render_wall"] = {"c2_1spp": cli_wall(False, local_rank), "c5_adaptive": cli_wall(True, local_rank)}
@@ -604,6 +627,10 @@ def main() -> None:
     ap.add_argument("--single-launches", type=int, default=2,
                     help="c2: frames rendered alone after the timed region (frac_single_launch)")
     ap.add_argument("--no-cli-wall", action="store_true", help="c2: skip the grt CLI wall-clock runs")
+    ap.add_argument("--arith", choices=("exact", "fused"), default="exact",
+                    help="grt_set_arithmetic for the timed loop (exact: the reference's roundings)")
+    ap.add_argument("--no-fused-check", dest="fused_check", action="store_false",
+                    help="c2, one GPU: skip the extra fused-mode measurement")
     ap.add_argument("--self-gather", action="store_true", help="c2, one GPU: run the multi-GPU gather path "
                     "in a process group of one (a check of the streams and RCCL gathers)")
     args = ap.parse_args()
@@ -628,9 +655,11 @@ def main() -> None:
 
     if args.blocks_per_cu:
         L.check(L.lib().grt_set_launch_config(args.blocks_per_cu, 256), "grt_set_launch_config")
+    L.check(L.lib().grt_set_arithmetic(1 if args.arith == "fused" else 0), "grt_set_arithmetic")
     line = (run_c4 if args.workload == "c4" else run_c2)(args, rank, world, local_rank, dev)
     if line is not None:
         line["source_hash"] = L.source_stamp()  # the sources libgrt.so was built from (checked on load)
+        line["arith"] = args.arith
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -11,7 +11,7 @@ from .scene import (  # noqa: F401
     BlackBody, Bitmap, Checker, GlobalOpts, HostScene, RenderResult, Scene, SceneBuilder, blackbody_xyz,
     build_camera, cartesian_to_boyer_lindquist, cartesian_to_spherical, default_adaptive, device_count,
     kerr_temperature_lut, load_scene, r_isco, srgb_to_xyza, stationary_velocity, xyz_to_srgb8, Trajectories, ray_at,
-    write_trajectory_csv, format_f64,
+    write_trajectory_csv, format_f64, set_arithmetic, get_arithmetic,
 )
 
 __all__ = [
@@ -19,4 +19,5 @@ __all__ = [
     "SceneBuilder", "blackbody_xyz", "build_camera", "cartesian_to_boyer_lindquist", "cartesian_to_spherical",
     "default_adaptive", "device_count", "kerr_temperature_lut", "load_scene", "r_isco", "srgb_to_xyza",
     "stationary_velocity", "xyz_to_srgb8", "Trajectories", "ray_at", "write_trajectory_csv", "format_f64",
+    "set_arithmetic", "get_arithmetic",
 ]

@@ -253,6 +253,8 @@ def lib() -> C.CDLL:
                                              C.POINTER(FrameOut), C.POINTER(C.c_uint64), C.POINTER(Stats),
                                              C.POINTER(SubsampleFailures), C.POINTER(MultiReport)]),
         "grt_multi_release": (None, []),
+        "grt_set_arithmetic": (C.c_int, [C.c_int]),
+        "grt_get_arithmetic": (C.c_int, []),
     }
     # GRT_LIB_ALLOW_MISSING=1 (tools/time_variants.py only) binds an older experimental
     # build that lacks newer entry points; by default a missing symbol is an error.
@@ -300,6 +302,7 @@ EXPORTED_SYMBOLS = [
     "grt_ray_at", "grt_write_trajectory_csv", "grt_format_f64", "grt_adaptive_min_luminance", "grt_adaptive_min_luminance_device", "grt_supersample_shard",
     "grt_supersample_shard_device", "grt_adaptive_floor_device", "grt_render_section_ex",
     "grt_write_png_rgb", "grt_write_hdr_xyz", "grt_render_frame_multi", "grt_multi_release",
+    "grt_set_arithmetic", "grt_get_arithmetic",
 ]
 
 

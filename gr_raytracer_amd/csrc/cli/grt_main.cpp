@@ -18,7 +18,8 @@
 // resolves texture paths, --raw-out FILE dumps the f64 XYZA buffer; --gpus N (GPUs
 // 0..N-1) or --devices A,B,... renders the whole frame over several GPUs of this process
 // (grt_render_frame_multi: cyclic row bands of --band-rows rows, default 16, one RCCL
-// gather), --gpus 1 included.
+// gather), --gpus 1 included; --arithmetic exact|fused selects grt_set_arithmetic (exact,
+// the reference's roundings, by default).
 #include <algorithm>
 #include <charconv>
 #include <chrono>
@@ -30,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "grt_api.h"
@@ -288,6 +290,11 @@ int main(int argc, char** argv) {
       }
       continue;
     }
+    if (a == "--arithmetic") {
+      if (v != "exact" && v != "fused") return bad();
+      (void)grt_set_arithmetic(v == "fused" ? 1 : 0);
+      continue;
+    }
     if (a == "--band-rows") {
       if (!int_in(1, 4294967295ull, &iv)) return bad();
       band_rows = (uint32_t)iv;
@@ -402,6 +409,15 @@ int main(int argc, char** argv) {
     filename = action == "render" ? "render.png" : (action == "render-ray" ? "rendered-ray.csv" : "rendered-ray-at.csv");
   if (config_file.empty()) return usage("Config file is required for this action");
 
+  // The HIP runtime's start-up (driver and device enumeration) runs beside the scene load
+  // below: the first HIP call of the process does it, wherever it is made.
+  std::thread hip_init([] { (void)grt_device_count(); });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } hip_init_join{hip_init};
   // phase times of a render (printed on one [grt] line at the end; not in the reference)
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
@@ -425,6 +441,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   ph_create = ms_since(t_phase);
+  hip_init.join();
   const grt_scene_desc* d = grt_host_scene_desc(hs);
   auto elapsed = [&]() {  // main.rs:175-176
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();

@@ -34,15 +34,18 @@ std::atomic<int> g_range_free{1};      // grt_debug_range_free: 0 = every divisi
 std::atomic<int> g_schedule{-1};       // grt_set_schedule: -1 auto, 0 row-major tiles, 1 probe-ordered tiles
 std::atomic<int> g_two_ended{1};       // grt_set_two_ended: probe-ordered traces take the queue from both ends
 std::atomic<long long> g_tail{-1};     // grt_set_tail: -1 auto, 0 off, > 0 hand-off threshold (live rays)
+std::atomic<int> g_arith{0};           // grt_set_arithmetic: 0 exact (reference bits), 1 fused (FMA contraction)
 constexpr uint32_t PROBE_CAP = 32768;  // upper bound of the probe's step cap
 
 struct Knobs {
   int blocks_per_cu, threads, schedule, two_ended;
   long long tail;
+  int arith;
   static Knobs now() {
     const long long l = g_launch.load(std::memory_order_relaxed);
     return Knobs{(int)(l >> 16), (int)(l & 0xffff), g_schedule.load(std::memory_order_relaxed),
-                 g_two_ended.load(std::memory_order_relaxed), g_tail.load(std::memory_order_relaxed)};
+                 g_two_ended.load(std::memory_order_relaxed), g_tail.load(std::memory_order_relaxed),
+                 g_arith.load(std::memory_order_relaxed)};
   }
 };
 
@@ -705,8 +708,12 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   rc = tail_list(s, dc, blocks * (uint64_t)threads, k.tail, &tl, &tail_blocks);
   if (rc) return rc;
   if (tl.cap) HIP_TRY(hipMemsetAsync(dc.d_tail_ctl, 0, 16 * sizeof(unsigned long long), stream));
-  HIP_TRY(grt::launch_trace(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads,
-                            dc.vol, tl, tail_blocks, stream));
+  // grt_set_arithmetic(1): the light charts' kernels built with FMA contraction
+  // (geodesic_fused.hip); Kerr-Schild always runs the exact ones
+  const bool fused = k.arith == 1 && s->desc.geometry != GRT_GEOM_KERR;
+  HIP_TRY((fused ? grt::fused::launch_trace : grt::launch_trace)(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter,
+                                                                  d_stats, blocks, threads, dc.vol, tl, tail_blocks,
+                                                                  stream));
   return stream_done(dc, stream);
 }
 
@@ -954,6 +961,14 @@ int grt_debug_range_free(int on) {
   g_range_free.store(on);
   return 0;
 }
+
+int grt_set_arithmetic(int mode) {
+  if (mode != 0 && mode != 1) return fail(-EINVAL, "arithmetic: 0 (exact) or 1 (fused)");
+  g_arith.store(mode);
+  return 0;
+}
+
+int grt_get_arithmetic(void) { return g_arith.load(); }
 
 int grt_set_two_ended(int on) {
   if (on != 0 && on != 1) return fail(-EINVAL, "two-ended queue: 0 or 1");

@@ -33,9 +33,21 @@
 #include "glibc_math.h"
 #include "kernels.h"
 
-namespace grt {
+// GRT_FUSED: this file compiled a second time, by geodesic_fused.hip, with FMA contraction
+// (-ffp-contract=fast) into namespace grt::fused: the trace kernels of the light charts
+// for grt_set_arithmetic(1).  Only launch_trace is defined there (Kerr-Schild excluded).
+#ifndef GRT_FUSED
+#define GRT_FUSED 0
+#endif
 
+namespace grt {
+#if GRT_FUSED
+namespace fused {
+#endif
+
+#ifndef GDEV
 #define GDEV __device__ __forceinline__
+#endif
 
 #ifndef GRT_SHARED_DIV
 #define GRT_SHARED_DIV 1
@@ -234,6 +246,7 @@ GDEV double ksqrt(double x) {
   else return sqrt(x);
 }
 
+#if !GRT_FUSED
 // Device check of div_inrange / div2_inrange / div_fx / sqrt_fx against the compiler's
 // division and sqrt over the whole exponent plane (tests/test_gpu_parity.py
 // ::test_range_free_arithmetic_map): thread (ex, ey), ex, ey biased exponents 0 .. 2046
@@ -288,6 +301,7 @@ __global__ void arith_map_kernel(uint32_t samples, uint64_t seed, uint8_t* map, 
   if (ex == 0) zmap[ey] = (uint8_t)zflags;
   if (ey == 0) smap[ex] = (uint8_t)sflags;
 }
+#endif  // !GRT_FUSED
 
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
@@ -1765,7 +1779,9 @@ GDEV unsigned long long hw_place() {
   const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
   return ((unsigned long long)xcc << 32) | hw;
 }
+#if !GRT_FUSED
 hipError_t set_ray_times(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_ray_times), &p, sizeof(p)); }
+#endif
 #define RAY_TIME(n, idx, k, v) ray_time(n, idx, k, v)
 #else
 #define RAY_TIME(n, idx, k, v) ((void)0)
@@ -2427,6 +2443,7 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
   }
 }
 
+#if !GRT_FUSED  // trajectories, monitors, probes and test hooks: exact build only
 // ======================================================= trajectory kernel =======
 // Integrator::integrate with the whole Vec<Step> kept (integrator.rs:78-174), the path
 // of `render-ray` / `render-ray-at` (main.rs:117-171, ray.rs:35-54).  One lane per ray;
@@ -2925,6 +2942,8 @@ hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& w
   return hipGetLastError();
 }
 
+
+#endif  // !GRT_FUSED
 // ============================================================ shade kernel =======
 // Evaluate one recorded candidate: the emitter step at the intersection
 // (objects.rs:27-44 + :95-115), its redshift, temperature and texture colour.
@@ -3312,9 +3331,11 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
     case GRT_GEOM_SCHWARZSCHILD:
       return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
                                               tail_blocks, stream);
+#if !GRT_FUSED  // Kerr-Schild always runs exact (grt_set_arithmetic)
     case GRT_GEOM_KERR:
       return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl, tail_blocks,
                                      stream);
+#endif
     case GRT_GEOM_KERR_BL:
       return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
                                         tail_blocks, stream);
@@ -3326,4 +3347,7 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
   }
 }
 
+#if GRT_FUSED
+}  // namespace fused
+#endif
 }  // namespace grt

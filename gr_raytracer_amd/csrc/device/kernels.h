@@ -55,6 +55,14 @@ hipError_t launch_rhs_check(int geometry, const DevScene* d_scene, const double*
 #if GRT_PATH_COUNT
 hipError_t path_read(unsigned long long* out, bool reset);  // 16 words
 #endif
+// The same trace compiled with FMA contraction (geodesic_fused.hip, grt_set_arithmetic(1)):
+// every geometry but Kerr-Schild (hipErrorInvalidValue for it).
+namespace fused {
+hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
+                        const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
+                        int blocks, int threads, bool vol, const TailList& tl, int tail_blocks,
+                        hipStream_t stream);
+}  // namespace fused
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
 
 // Invariant monitors of the n = rows x cols rays of a rectangle (health_kernel):

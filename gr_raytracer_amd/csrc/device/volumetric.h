@@ -162,22 +162,37 @@ GDEV bool vdisc_chord(const DevObject& o, const double* s, const double* e, doub
 //   h   0..7: u = x        8..11: u = y      12,13: u = x      14,15: u = y
 //   v   0..3: y   4..11: z   12,13: y   14,15: z;   -u: h odd or h >= 14;
 //   -v: (h & 2) for h < 12, and h == 15.   (-x) + y etc. are exact negations.
-GDEV double grad_dot(uint32_t h, double x, double y, double z) {
+GDEV double s_curve5(double x) { return x * x * x * (x * (x * 6.0 - 15.0) + 10.0); }
+
+// grad_dot as coefficients: hash h picks (gx, gy, gz) in {-1, 0, +1}, two of them non-zero
+// (+-u +- v above), and gradient_dot_v is fma(gz, z, fma(gy, y, gx * x)).  Each product
+// is exact (x, -x or a zero), so the two fused adds round the exact sum +-u +- v once, as
+// the reference's one addition does: the same value, except that a zero result may carry
+// the other sign.  That never reaches the density: every perlin value only enters the
+// fBm sum n, which starts at +0.0 and is never -0.0, and x + (+-0) is x for every x != 0
+// and +0 for x = +0.  The march kernel keeps the 16 rows in LDS (one read of a 32-B row
+// per corner instead of ~26 integer / select instructions of grad_dot).
+GDEV double grad_coef(uint32_t h, uint32_t axis) {
   h &= 15u;
-  const double u = (h < 8u || h == 12u || h == 13u) ? x : y;
-  const double v = (h < 4u || h == 12u || h == 13u) ? y : z;
+  const uint32_t u_axis = (h < 8u || h == 12u || h == 13u) ? 0u : 1u;
+  const uint32_t v_axis = (h < 4u || h == 12u || h == 13u) ? 1u : 2u;
   const bool nu = (h & 1u) || h >= 14u;
   const bool nv = h < 12u ? (h & 2u) != 0u : h == 15u;
-  return (nu ? -u : u) + (nv ? -v : v);
+  if (axis == u_axis) return nu ? -1.0 : 1.0;
+  if (axis == v_axis) return nv ? -1.0 : 1.0;
+  return 0.0;
 }
-GDEV double s_curve5(double x) { return x * x * x * (x * (x * 6.0 - 15.0) + 10.0); }
+GDEV double grad_dot_lds(const double* __restrict__ G, uint32_t h, double x, double y, double z) {
+  const double* g = G + ((h & 15u) << 2);
+  return __builtin_fma(g[2], z, __builtin_fma(g[1], y, g[0] * x));
+}
 
 // (corner as isize) & 0xff of an integral double: fl - 256 floor(fl / 256) is exact
 // (power-of-two scaling, integral operands below 2^53) and lies in [0, 255]; the
 // reference's numcast() panics beyond the isize range, where this is never reached.
 GDEV uint32_t lattice_byte(double fl) { return (uint32_t)(int32_t)__builtin_fma(-256.0, floor(fl * 0.00390625), fl); }
 
-GDEV double perlin3(const uint8_t* P, double px, double py, double pz) {
+GDEV double perlin3(const uint8_t* P, const double* G, double px, double py, double pz) {
   const double fx = floor(px), fy = floor(py), fz = floor(pz);
   const double dx = px - fx, dy = py - fy, dz = pz - fz;
   const uint32_t x0 = lattice_byte(fx), x1 = (x0 + 1u) & 0xffu;
@@ -186,14 +201,14 @@ GDEV double perlin3(const uint8_t* P, double px, double py, double pz) {
   const uint32_t a0 = P[x0], a1 = P[x1];
   const uint32_t b00 = P[a0 ^ y0], b10 = P[a1 ^ y0], b01 = P[a0 ^ y1], b11 = P[a1 ^ y1];
   const double dx1 = dx - 1.0, dy1 = dy - 1.0, dz1 = dz - 1.0;
-  const double g000 = grad_dot(P[b00 ^ z0], dx, dy, dz);
-  const double g100 = grad_dot(P[b10 ^ z0], dx1, dy, dz);
-  const double g010 = grad_dot(P[b01 ^ z0], dx, dy1, dz);
-  const double g110 = grad_dot(P[b11 ^ z0], dx1, dy1, dz);
-  const double g001 = grad_dot(P[b00 ^ z1], dx, dy, dz1);
-  const double g101 = grad_dot(P[b10 ^ z1], dx1, dy, dz1);
-  const double g011 = grad_dot(P[b01 ^ z1], dx, dy1, dz1);
-  const double g111 = grad_dot(P[b11 ^ z1], dx1, dy1, dz1);
+  const double g000 = grad_dot_lds(G, P[b00 ^ z0], dx, dy, dz);
+  const double g100 = grad_dot_lds(G, P[b10 ^ z0], dx1, dy, dz);
+  const double g010 = grad_dot_lds(G, P[b01 ^ z0], dx, dy1, dz);
+  const double g110 = grad_dot_lds(G, P[b11 ^ z0], dx1, dy1, dz);
+  const double g001 = grad_dot_lds(G, P[b00 ^ z1], dx, dy, dz1);
+  const double g101 = grad_dot_lds(G, P[b10 ^ z1], dx1, dy, dz1);
+  const double g011 = grad_dot_lds(G, P[b01 ^ z1], dx, dy1, dz1);
+  const double g111 = grad_dot_lds(G, P[b11 ^ z1], dx1, dy1, dz1);
   const double a = s_curve5(dx), b = s_curve5(dy), c = s_curve5(dz);
   const double k0 = g000;
   const double k1 = g100 - g000;
@@ -214,7 +229,8 @@ GDEV double perlin3(const uint8_t* P, double px, double py, double pz) {
 struct PlaneAngle {
   double x, y, sp, cp;
 };
-GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p, PlaneAngle* pa, bool* noise) {
+GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const double* G, const V3& p, PlaneAngle* pa,
+                          bool* noise) {
   *noise = false;
   const V3 ax = vaxis(o);
   const double h = fabs(vdot(p, ax));
@@ -238,11 +254,11 @@ GDEV double vdisc_density(const DevObject& o, const uint8_t* P, const V3& p, Pla
   const double npx = r * o.ns[0], npy = cp * o.ns[1], npz = sp * o.ns[1];
   double n = 0.0, frequency = 4.0, amplitude = 1.0;  // fbm (:330-342)
   for (uint32_t i = 0; i < o.octaves; ++i) {
-    n += amplitude * perlin3(P, npx * frequency, npy * frequency, npz * frequency);
+    n += amplitude * perlin3(P, G, npx * frequency, npy * frequency, npz * frequency);
     frequency *= 2.0;
     amplitude *= o.g_fbm;
   }
-  n += perlin3(P, r * 0.5, h * o.ns[2], cp) * 0.5;
+  n += perlin3(P, G, r * 0.5, h * o.ns[2], cp) * 0.5;
   const double n2 = fmax(n + o.noff, 0.0) * o.dens_mult;
   return n2 * radial_base * vertical_falloff * boundary_falloff;
 }
@@ -324,6 +340,8 @@ template <int G>
 __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restrict__ Sp, Workspace ws) {
   const DevScene& S = *Sp;
   __shared__ uint8_t lds_perm[GRT_MAX_OBJECTS * 256];
+  __shared__ double lds_grad[16 * 4];  // grad_coef rows (gx, gy, gz, 0), 32 B each
+  if (threadIdx.x < 64) lds_grad[threadIdx.x] = (threadIdx.x & 3u) == 3u ? 0.0 : grad_coef(threadIdx.x >> 2, threadIdx.x & 3u);
   __shared__ double lds_tr[MARCH_LUT_MAX], lds_tt[MARCH_LUT_MAX];
   __shared__ double lds_bt[MARCH_LUT_MAX], lds_bx[3 * MARCH_LUT_MAX];
   for (unsigned i = threadIdx.x; i < GRT_MAX_OBJECTS * 256u; i += blockDim.x) lds_perm[i] = S.perm[i >> 8][i & 255u];
@@ -435,7 +453,7 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
     bool failed = false;
     PlaneAngle pa;
     bool noise;
-    const double density = vdisc_density(o, P, p, &pa, &noise);
+    const double density = vdisc_density(o, P, lds_grad, p, &pa, &noise);
     n_noise += noise ? 1u : 0u;
     if (density > 0.0) {
       const double sig = o.sig_a + o.sig_s;

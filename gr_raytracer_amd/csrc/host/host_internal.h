@@ -4,7 +4,9 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "grt_api.h"
@@ -12,6 +14,24 @@
 namespace grt_host {
 
 void set_error(const std::string& msg);
+// fn(i) for i in [0, n) on up to 16 host threads (interleaved); fn must only write its own i.
+// Setup loops whose entries are independent (LUTs), so every entry is the same value as in
+// a sequential loop.
+template <class F>
+void parallel_for(uint64_t n, F&& fn) {
+  const unsigned hw = std::thread::hardware_concurrency();
+  const unsigned nt = (unsigned)std::min<uint64_t>(n, std::max(1u, std::min(16u, hw)));
+  if (nt <= 1) {
+    for (uint64_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (unsigned k = 0; k < nt; ++k)
+    pool.emplace_back([&, k] {
+      for (uint64_t i = k; i < n; i += nt) fn(i);
+    });
+  for (auto& t : pool) t.join();
+}
 // The camera frame of a device scene (grt_scene_desc.camera rows x cols; api.hip).
 void scene_frame_size(const grt_scene* s, int64_t* rows, int64_t* cols);
 double rclamp_pub(double v, double lo, double hi);

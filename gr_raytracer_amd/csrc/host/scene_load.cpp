@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <future>
 #include <memory>
 #include <map>
 #include <sstream>
@@ -23,6 +24,15 @@ struct CachedTexture {
   uint32_t w = 0, h = 0;
   double beaming = 0.0;
   std::vector<uint8_t> rgba;
+  // the PNG decode, started when the texture is first named and waited for at the end of
+  // grt_host_scene_load (the textures decode beside each other and beside the LUTs);
+  // the decode's error text, "" when it succeeded
+  std::shared_future<std::string> decoded;
+};
+// A texture descriptor waiting for its bitmap's size and texels.
+struct TexturePatch {
+  grt_texture_desc* d;
+  CachedTexture* ct;
 };
 struct grt_host_scene {
   grt_scene_desc desc;
@@ -160,7 +170,8 @@ std::string join_path(const char* root, const std::string& p) {
 
 using namespace grt_host;
 
-static int fill_texture(grt_host_scene* hs, const TexSpec& t, const char* root, grt_texture_desc& d, bool* need_bb) {
+static int fill_texture(grt_host_scene* hs, const TexSpec& t, const char* root, grt_texture_desc& d, bool* need_bb,
+                        std::vector<TexturePatch>* patches) {
   std::memset(&d, 0, sizeof(d));
   d.kind = t.kind;
   d.beaming_exponent = t.beaming;
@@ -170,16 +181,18 @@ static int fill_texture(grt_host_scene* hs, const TexSpec& t, const char* root, 
     auto it = hs->textures.find(t.path);
     if (it == hs->textures.end()) {
       std::unique_ptr<CachedTexture> ct(new CachedTexture());
-      std::string err;
-      if (!png_decode_rgba(join_path(root, t.path), ct->rgba, ct->w, ct->h, err)) return fail(err);
+      CachedTexture* c = ct.get();
+      const std::string path = join_path(root, t.path);
+      c->decoded = std::async(std::launch::async, [c, path]() {
+                     std::string err;
+                     return png_decode_rgba(path, c->rgba, c->w, c->h, err) ? std::string() : err;
+                   }).share();
       ct->beaming = t.beaming;
       it = hs->textures.emplace(t.path, std::move(ct)).first;
     }
-    const CachedTexture& ct = *it->second;
-    d.width = ct.w;
-    d.height = ct.h;
-    d.rgba = ct.rgba.data();
-    d.beaming_exponent = ct.beaming;
+    // size and texels once the decode is done (grt_host_scene_load's end)
+    patches->push_back(TexturePatch{&d, it->second.get()});
+    d.beaming_exponent = it->second->beaming;
   } else if (t.kind == GRT_TEX_CHECKER) {
     d.checker_width = t.cw;
     d.checker_height = t.ch;
@@ -358,7 +371,8 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
   bool need_bb = false;
   TexSpec ct;
   if (!parse_texture(get(root, "celestial_texture"), ct, err)) return fail("celestial_texture: " + err);
-  int rc = fill_texture(hs.get(), ct, resource_root, d.celestial, &need_bb);
+  std::vector<TexturePatch> patches;
+  int rc = fill_texture(hs.get(), ct, resource_root, d.celestial, &need_bb, &patches);
   if (rc) return rc;
   if (!num(root, "celestial_temperature", &d.celestial_temperature, err)) return fail(err);
   rc = grt_camera_build(d.geometry, d.radius, d.a, pos, vel, 3.14159265358979323846 / 4.0, opts->height, opts->width,
@@ -450,7 +464,7 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
     } else {
       return fail("unknown object `" + oname + "`");
     }
-    rc = fill_texture(hs.get(), tex, resource_root, o.texture, &need_bb);
+    rc = fill_texture(hs.get(), tex, resource_root, o.texture, &need_bb, &patches);
     if (rc) return rc;
     d.n_objects++;
   }
@@ -461,6 +475,14 @@ int grt_host_scene_load(const char* toml_path, const char* resource_root, const 
     d.bb_log_t = hs->bb_log_t.data();
     d.bb_xyz = hs->bb_xyz.data();
     d.bb_n = 1000;
+  }
+  // the bitmaps, in the order the scene names them (the first decode error is reported)
+  for (const TexturePatch& p : patches) {
+    const std::string& err = p.ct->decoded.get();
+    if (!err.empty()) return fail(err);
+    p.d->width = p.ct->w;
+    p.d->height = p.ct->h;
+    p.d->rgba = p.ct->rgba.data();
   }
   *out = hs.release();
   return 0;

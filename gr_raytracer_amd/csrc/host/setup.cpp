@@ -738,13 +738,18 @@ int kerr_temperature_lut(double temperature, double outer_radius, double a, doub
     *log += "Computed m_dot: " + rust_display_f64(kt.m_dot) + " for target temperature: " +
             rust_display_f64(temperature) + "\n";
   double step = (eff_outer - ri) / (double)(n - 1);
-  for (uint32_t i = 0; i < n; ++i) {
+  // the entries are independent (each its own integral): host threads, the first failing
+  // entry's error in index order, as the reference's sequential loop would return it
+  std::vector<int> rcs(n, 0);
+  parallel_for(n, [&](uint64_t i) {
     double r = ri + (double)i * step;
     double fv;
-    if ((rc = kt.compute_f(r, &fv))) return rc;
+    if ((rcs[i] = kt.compute_f(r, &fv))) return;
     lut_r[i] = r;
     lut_t[i] = std::pow(std::fmax(fv / sigma_sb, 0.0), 0.25);
-  }
+  });
+  for (uint32_t i = 0; i < n; ++i)
+    if (rcs[i]) return rcs[i];
   *r_isco_out = ri;
   return 0;
 }
@@ -823,12 +828,12 @@ int blackbody_lut(uint32_t n, double* log_t, double* xyz) {  // texture.rs:121-1
   if (n < 2) return -EINVAL;
   double min_log = std::log10(10.0), max_log = std::log10(10000000.0);
   double step = (max_log - min_log) / (double)(n - 1);
-  for (uint32_t i = 0; i < n; ++i) {
+  parallel_for(n, [&](uint64_t i) {  // independent entries
     double lt = min_log + (double)i * step;
     double t = std::pow(10.0, lt);
     log_t[i] = lt;
     blackbody_xyz(t, 1.0, xyz + 3 * i);
-  }
+  });
   return 0;
 }
 

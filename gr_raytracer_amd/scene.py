@@ -421,6 +421,20 @@ def set_two_ended(on: bool = True) -> None:
     L.check(L.lib().grt_set_two_ended(1 if on else 0), "grt_set_two_ended")
 
 
+ARITH_EXACT, ARITH_FUSED = 0, 1
+
+
+def set_arithmetic(mode) -> None:
+    """grt_set_arithmetic: "exact" / 0 (the reference's roundings, default) or "fused" / 1
+    (FMA contraction in the light charts' kernels; Kerr-Schild stays exact)."""
+    m = {"exact": 0, "fused": 1}.get(mode, mode)
+    L.check(L.lib().grt_set_arithmetic(int(m)), "grt_set_arithmetic")
+
+
+def get_arithmetic() -> int:
+    return int(L.lib().grt_get_arithmetic())
+
+
 def set_tail(threshold: int = -1) -> None:
     """Long-ray hand-off of Kerr-Schild traces (grt_set_tail): -1 auto, 0 off, > 0 the
     live-ray threshold.  Scheduling only; results are identical in every mode."""

@@ -649,6 +649,19 @@ int grt_tonemap_async(int device, void* stream, const double* d_xyza, uint64_t n
 int grt_xyz_to_srgb8_device(int device, const double* xyza, size_t n, int32_t tone_mapping,
                             double exposure, uint8_t* rgb_out);
 
+/* Floating-point contraction of the trace (no reference counterpart: the reference's Rust
+ * never fuses a*b + c).  0 = exact (default): every multiply and add rounded separately in
+ * the reference's order, so pixels are bit-identical to the reference's wherever the libm
+ * calls are.  1 = fused: the light charts (Euclidean, Schwarzschild,
+ * KerrBL, EuclideanSpherical) run kernels compiled with FMA contraction -- the same
+ * algorithm and operation order, one rounding per fused pair -- which is faster (C2 -17%,
+ * C3 -13%) and keeps every robust pixel within the north-star 1e-4 relative per channel
+ * (tests/test_fused.py), but no longer bit-identical; Kerr-Schild always runs exact (its
+ * finite-difference metric turns the changed roundings into other step sequences).
+ * Process-wide; each trace reads it once when it is enqueued. */
+int grt_set_arithmetic(int mode);
+int grt_get_arithmetic(void);
+
 /* Kernel launch geometry knobs (persistent grid). 0 = library default: 256 threads per
  * block, 2w blocks per CU for an integrate kernel that keeps w waves per SIMD resident
  * (w = 3 for Schwarzschild, KerrBL and the flat charts; 2 for Kerr-Schild and scenes with

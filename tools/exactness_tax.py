@@ -91,7 +91,33 @@ def c4():
     return out
 
 
+def c5_save(path):
+    """C5 (stock adaptive 4x4) frame of this library, saved for c5_compare."""
+    hs = host_scene(g, "schwarzschild.toml", c2_opts(g))
+    sc = gpu_scene(g, hs)
+    r = sc.render_section_ex(adaptive=hs.adaptive)
+    np.savez(path, xyza64=r.xyza64, cls=r.ray_class, n_sel=r.n_supersampled)
+    return {"config": "C5 saved", "path": path, "n_supersampled": r.n_supersampled, "kernel_ms": r.stats["kernel_ms"]}
+
+
+def c5_compare(a, b):
+    """Pixels of two C5 frames outside 1e-4 (relative per channel) of each other."""
+    from test_gpu_parity import within
+
+    A, B = np.load(a), np.load(b)
+    ok = within(B["xyza64"], A["xyza64"]) & (A["cls"] == B["cls"])
+    return {"config": "C5 compare", "pixels": int(ok.size), "within_1e-4": int(ok.sum()), "outside": int((~ok).sum()),
+            "n_supersampled": [int(A["n_sel"]), int(B["n_sel"])],
+            "exact": int(np.all(A["xyza64"] == B["xyza64"], axis=1).sum())}
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["C5save"]:
+        print(json.dumps(c5_save(sys.argv[2])), flush=True)
+        sys.exit(0)
+    if sys.argv[1:2] == ["C5compare"]:
+        print(json.dumps(c5_compare(sys.argv[2], sys.argv[3])), flush=True)
+        sys.exit(0)
     which = sys.argv[1:] or ["C1", "C2", "C3", "C4"]
     lib = os.environ.get("GRT_LIB", "in-tree")
     for w in which:

@@ -5,6 +5,7 @@ For each scene: one warm-up and two timed 1-spp frames through grt_render_pixels
 outputs), printing accepted RKF45 steps, raymarch jobs / samples and the kernel time
 (HIP events around integrate + job gather + march + composite), as one JSON line each.
 """
+import hashlib
 import json
 import sys
 import time
@@ -42,6 +43,7 @@ def main():
                           "march_samples": st["march_samples"], "march_noise_samples": st["march_noise_samples"],
                           "march_emit_samples": st["march_emit_samples"],
                           "hit_pixels": int((r.ray_class == 2).sum()),
+                          "md5": hashlib.md5(r.xyza.tobytes() + r.ray_class.tobytes()).hexdigest()[:12],
                           "march_samples_per_s": st["march_samples"] / (st["kernel_ms"] * 1e-3)}), flush=True)
 
 
