@@ -60,7 +60,8 @@ def fused_parity(oracle, desc, cols, ri, ci, got, max_outside=0.02):
         assert wrong.size == 0, f"{wrong.size} robust pixels outside 1e-4, e.g. {list(zip(ri[wrong[:4]], ci[wrong[:4]]))}"
         robust[suspect] = False
     assert np.array_equal(got["stop"][robust], ref["stop"][robust])
-    return ok.mean()
+    bit_exact = np.all(got["xyza64"] == ref["xyza"], axis=1).mean()
+    return ok.mean(), bit_exact
 
 
 def sample_frame(sc, cell, seed):
@@ -77,7 +78,8 @@ def test_fused_c1_whole_frame(grt, oracle, gpu, fused):
     hs = host_scene(grt, "euclidean.toml", grt.GlobalOpts(width=256, height=256))
     sc = gpu_scene(grt, hs)
     full, ri, ci, got = sample_frame(sc, 1, 0)
-    assert fused_parity(oracle, hs.desc, sc.cols, ri, ci, got, max_outside=0.0) == 1.0
+    within, bit_exact = fused_parity(oracle, hs.desc, sc.cols, ri, ci, got, max_outside=0.0)
+    assert within == 1.0 and bit_exact < 0.9  # every pixel within 1e-4, most with other last bits
 
 
 @pytest.mark.gpu
@@ -89,7 +91,8 @@ def test_fused_whole_frame_sample(grt, oracle, gpu, fused, config):
     hs = host_scene(grt, toml, opts)
     sc = gpu_scene(grt, hs)
     full, ri, ci, got = sample_frame(sc, cell, 11)
-    assert fused_parity(oracle, hs.desc, sc.cols, ri, ci, got) >= 0.98
+    within, bit_exact = fused_parity(oracle, hs.desc, sc.cols, ri, ci, got)
+    assert within >= 0.98 and bit_exact < 0.9
     # the f32 framebuffer is still the f64 colour rounded once
     assert np.array_equal(full.xyza, full.xyza64.astype(np.float32))
 
@@ -98,20 +101,21 @@ def test_fused_whole_frame_sample(grt, oracle, gpu, fused, config):
 def test_fused_mode_differs_from_exact_and_keeps_kerr_schild_exact(grt, gpu):
     import bench
 
-    hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt))
+    hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=256, height=256))
     sc = gpu_scene(grt, hs)
-    rect = (700, 700, 64, 64)
-    exact = sc.render_pixels(*rect)
+    exact = sc.render_pixels()
     grt.set_arithmetic("fused")
     try:
-        fz = sc.render_pixels(*rect)
+        fz = sc.render_pixels()
         hk = host_scene(grt, "kerr.toml", bench.c4_opts(grt, 512, max_steps=100000))
         sk = gpu_scene(grt, hk)
         k_fused = sk.render_pixels(192, 192, 96, 96)
     finally:
         grt.set_arithmetic("exact")
     k_exact = sk.render_pixels(192, 192, 96, 96)
-    assert not np.array_equal(fz.xyza64, exact.xyza64)  # the fused kernels ran
+    # the fused kernels ran: other last bits on most sky and disc pixels, the same pixels
+    differ = np.any(fz.xyza64 != exact.xyza64, axis=1)
+    assert differ.mean() > 0.1, differ.mean()
     assert np.array_equal(k_fused.xyza64.view(np.uint64), k_exact.xyza64.view(np.uint64))
     assert np.array_equal(k_fused.steps, k_exact.steps)
 
