@@ -435,6 +435,9 @@ def run_c2(args, rank, world, local_rank, dev):
                              "<0.01%)"),
         "cpu_baseline": None,
     }
+    # each timed frame's own span between its two events on its slot's stream (with frames in
+    # flight a span includes the time the frame shares the CUs with its neighbours)
+    line["roofline"]["frame_event_ms"] = [round(a.elapsed_time(b), 1) for a, b in ev]
     line["roofline"]["kernel_ms_basis"] = (
         "mean launch duration (HIP events on the launch stream)" if F == 1 else
         f"pipelined throughput: device time per frame with {F} frames in flight, first frame's start event to "

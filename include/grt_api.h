@@ -658,6 +658,8 @@ int grt_xyz_to_srgb8_device(int device, const double* xyza, size_t n, int32_t to
  * C3 -13%) and keeps every robust pixel within the north-star 1e-4 relative per channel
  * (tests/test_fused.py), but no longer bit-identical; Kerr-Schild always runs exact (its
  * finite-difference metric turns the changed roundings into other step sequences).
+ * It applies to frame traces (grt_render_*, grt_supersample_shard*, grt_render_frame_multi);
+ * trajectories (grt_trace_*), monitors and the work-order probe always run exact.
  * Process-wide; each trace reads it once when it is enqueued. */
 int grt_set_arithmetic(int mode);
 int grt_get_arithmetic(void);

@@ -9,7 +9,8 @@ the photon ring are sampled wherever they fall:
   one per 10 x 10 stratum-cell are traced by the oracle;
 * C3 (1500^2 kerr-bl.toml): as C2, 5 000 pixels;
 * C4 (4096^2 kerr.toml, Kerr-Schild, max-steps 1e6): 1 024 pixels, one per 128 x 128
-  cell, on both sides through the offsets mode at the pixel centre (dx = dy = 0.5 gives
+  cell, and 4 096 of another draw, one per 64 x 64 cell, on both sides through the
+  offsets mode at the pixel centre (dx = dy = 0.5 gives
   row + 0.0, the base ray: camera.rs:247-254, KAT in tests/test_oracle_kats.py);
 * C5 (1500^2 schwarzschild.toml, stock adaptive 4 x 4): the selected pixel set of
   grt_render_section equals the oracle's collect_pixels_to_supersample applied to the
@@ -113,13 +114,15 @@ def test_c3_whole_frame_sample(grt, oracle, gpu):
     assert n >= 5000
 
 
-def test_c4_whole_frame_sample(grt, oracle, gpu):
+@pytest.mark.parametrize("cell,seed", [(128, 13), (64, 17)])
+def test_c4_whole_frame_sample(grt, oracle, gpu, cell, seed):
     """configs[3]: 1 024 pixels of the 4096^2 Kerr-Schild frame, one per 128 x 128 cell,
-    traced in offsets mode at the pixel centre on both sides."""
+    and 4 096 more, one per 64 x 64 cell (another draw), traced in offsets mode at the
+    pixel centre on both sides."""
     hs = host_scene(grt, "kerr.toml", c4_opts(grt))
     sc = gpu_scene(grt, hs)
     cols = sc.cols
-    ri, ci = stratified(sc.rows, cols, 128, 13)
+    ri, ci = stratified(sc.rows, cols, cell, seed)
     pix = (ri * cols + ci).astype(np.uint32)
     half = np.full(len(pix), 0.5)
     g = sc.render_pixels(offsets=(pix, half, half))
