@@ -195,6 +195,61 @@ __global__ void frame_index_kernel(const uint32_t* __restrict__ sel_local, const
   sel_frame[j] = shard_frame_row(band_rows, shard, n_shards, i / w) * w + i % w;
 }
 
+static inline unsigned nblocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// Work order of the supersample pass, longest sub-rays first.  A pixel's sort key is the
+// most 1-spp steps in its 3 x 3 neighbourhood (its sub-rays sample the pixel's square,
+// between its own centre ray and its neighbours'), + 1 so that the unused entries (key 0)
+// sort last.  C5: the pass's lane occupancy 0.69 -> 0.78 and its end after the queue
+// drains 0.17 -> 0.10 s (tools/ray_timeline.py c5); C5 1,639-1,665 -> 1,604-1,621 ms, the
+// frame bit-identical (profiles/r06i).  The pixel's own steps as the key: no gain.
+__global__ void sub_order_keys_kernel(const uint32_t* __restrict__ sel, const unsigned long long* __restrict__ d_count,
+                                      uint64_t n_max, const uint32_t* __restrict__ steps, uint32_t w, uint32_t h,
+                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_max) return;
+  uint32_t key = 0, p = 0;
+  if (j < *d_count) {
+    p = sel[j];
+    const int row = (int)(p / w), col = (int)(p % w);
+    uint32_t m = steps[p];
+    for (int dr = -1; dr <= 1; ++dr)
+      for (int dc = -1; dc <= 1; ++dc) {
+        const int r = row + dr, c = col + dc;
+        if (r >= 0 && r < (int)h && c >= 0 && c < (int)w) m = max(m, steps[(uint64_t)r * w + c]);
+      }
+    key = m == 0xffffffffu ? m : m + 1;
+  }
+  keys[j] = key;
+  vals[j] = p;
+}
+
+hipError_t order_selection(const uint32_t* d_sel, const unsigned long long* d_count, uint64_t n_max,
+                           const uint32_t* d_steps, uint32_t w, uint32_t h, uint32_t* d_out, void* d_temp,
+                           size_t* temp_bytes, hipStream_t stream) {
+  if (n_max == 0 || n_max > (uint64_t)INT_MAX) return n_max ? hipErrorInvalidValue : hipSuccess;
+  const size_t arr = (n_max * 4 + 255) & ~(size_t)255;
+  size_t sort_bytes = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_bytes, (const uint32_t*)nullptr,
+                                                              (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                                              (uint32_t*)nullptr, (int)n_max, 0, 32, stream);
+  if (e != hipSuccess) return e;
+  if (d_temp == nullptr) {
+    *temp_bytes = 3 * arr + sort_bytes;
+    return hipSuccess;
+  }
+  uint32_t* keys = (uint32_t*)d_temp;
+  uint32_t* keys_sorted = (uint32_t*)((char*)d_temp + arr);
+  uint32_t* vals = (uint32_t*)((char*)d_temp + 2 * arr);
+  void* tmp = (char*)d_temp + 3 * arr;
+  hipLaunchKernelGGL(sub_order_keys_kernel, dim3(nblocks(n_max, 256)), dim3(256), 0, stream, d_sel, d_count, n_max,
+                     d_steps, w, h, keys, vals);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // a stable sort: equal keys keep the selection order
+  return hipcub::DeviceRadixSort::SortPairsDescending(tmp, sort_bytes, keys, keys_sorted, vals, d_out, (int)n_max, 0,
+                                                      32, stream);
+}
+
 // resolve_minimum_luminance's order (raytracer.rs:118-129): f64::total_cmp of the
 // luminance Y, as an unsigned radix key (total_cmp's signed key with the sign bit
 // flipped).  The map is its own inverse on the low 63 bits, so the selected key gives
@@ -209,8 +264,6 @@ __global__ void lum_keys_kernel(const double* __restrict__ y, uint32_t stride, u
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) keys[i] = total_cmp_ukey(y[(uint64_t)stride * i]);
 }
-
-static inline unsigned nblocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // 1e-3 x the index-th key (resolve_minimum_luminance, raytracer.rs:125-128), on the device
 __global__ void floor_kernel(const uint64_t* __restrict__ sorted, uint64_t index, double* __restrict__ d_min_lum) {

@@ -1577,11 +1577,16 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
   size_t sort_bytes = 0, select_bytes = 0;
   if (device_floor) HIP_TRY(grt::luminance_floor_device(nullptr, 4, n, floor_index(n), nullptr, &sort_bytes, nullptr, 0));
   if (supersampled) HIP_TRY(grt::compact_flags(nullptr, n, nullptr, nullptr, nullptr, &select_bytes, 0));
+  // the supersample pass's work order (longest sub-rays first) reads the 1-spp step counts
+  const bool ordered = supersampled && !mask_xyza;
+  size_t order_bytes = 0;
+  if (ordered) HIP_TRY(grt::order_selection(nullptr, nullptr, n, nullptr, w, h, nullptr, nullptr, &order_bytes, 0));
   const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
   const bool want_events = fail_cap && failures->stop;
   grt::SubsampleFailures fails{nullptr, nullptr, nullptr, fail_cap};
   uint8_t* b_stop = nullptr;
-  uint32_t* b_steps = nullptr;
+  uint32_t *b_steps = nullptr, *b_order = nullptr;
+  void* b_order_tmp = nullptr;
   auto carve = [&](AdArena& A, float** xyza, uint8_t** cls, uint8_t** status, double** x64, uint8_t** flags,
                    uint32_t** sel, unsigned long long** cnt, double** floor, void** sort, void** select,
                    SuperBufs* B) {
@@ -1590,8 +1595,12 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
     *status = (uint8_t*)A.take(n);
     *x64 = (double*)A.take(n * 32);
     if (stop_out) b_stop = (uint8_t*)A.take(n);
-    if (steps_out) b_steps = (uint32_t*)A.take(n * 4);
+    if (steps_out || ordered) b_steps = (uint32_t*)A.take(n * 4);
     if (!supersampled) return;
+    if (ordered) {
+      b_order = (uint32_t*)A.take(n * 4);
+      b_order_tmp = A.take(order_bytes);
+    }
     *flags = (uint8_t*)A.take(n);
     *sel = (uint32_t*)A.take(n * 4);
     *cnt = (unsigned long long*)A.take(16);  // [0] selected pixels, [1] failed sub-samples
@@ -1650,7 +1659,8 @@ int grt_render_section_ex(grt_scene* s, int device, uint32_t from_row, uint32_t 
       HIP_TRY(grt::launch_paint(b_sel, n, d_cnt, mask_xyza, b_x64, st));
     } else {
       fails.count = d_cnt + 1;
-      if ((rc = enqueue_supersample(s, *dc, st, B, from_row, from_col, h, w, b_sel, b_sel, d_cnt, spa, b_x64,
+      HIP_TRY(grt::order_selection(b_sel, d_cnt, n, b_steps, w, h, b_order, b_order_tmp, &order_bytes, st));
+      if ((rc = enqueue_supersample(s, *dc, st, B, from_row, from_col, h, w, b_order, b_order, d_cnt, spa, b_x64,
                                     dc->d_stats, fails)))
         return rc;
     }

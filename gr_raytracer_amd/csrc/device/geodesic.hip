@@ -1321,17 +1321,27 @@ GDEV XYZA texel(const DevScene& S, const DevTexture& t, uint32_t x, uint32_t y) 
   return c;
 }
 
+// The reference's table searches (binary search, then idx = partition point - 1) over a
+// sorted table a[0..n) with a[0] < x < a[n - 1]: the last idx with a[idx] <= x.  Both
+// tables are evenly spaced grids (host/setup.cpp: x0 + i * step), so the index is guessed
+// from the spacing and corrected by comparisons against the table itself: the same idx
+// for any sorted table (a poor guess only costs more steps), with two dependent loads
+// instead of the ~10 of the bisection.
+GDEV uint32_t lut_index(const double* a, uint32_t n, double a0, double a_last, double x) {
+  const double g = (x - a0) * ((double)(n - 1) / (a_last - a0));
+  uint32_t idx = g >= (double)(n - 2) ? n - 2 : (g > 0.0 ? (uint32_t)g : 0u);
+  while (idx < n - 2 && a[idx + 1] <= x) ++idx;
+  while (idx > 0 && a[idx] > x) --idx;
+  return idx;
+}
+
 // texture.rs:149-195 over a (log10 T, XYZ) table in global memory or LDS
 GDEV XYZA sample_blackbody_lut(const double* lt, const double* c, uint32_t n, double temperature) {
   double log_t = log10(fmax(temperature, 10.0));
-  if (!isfinite(log_t) || log_t <= lt[0]) return XYZA{c[0], c[1], c[2], 1.0};
-  if (log_t >= lt[n - 1]) return XYZA{c[3 * (n - 1)], c[3 * (n - 1) + 1], c[3 * (n - 1) + 2], 1.0};
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    uint32_t mid = lo + (hi - lo) / 2;
-    if (lt[mid] <= log_t) lo = mid + 1; else hi = mid;
-  }
-  uint32_t idx = lo == 0 ? 0 : lo - 1;
+  const double lt_first = lt[0], lt_last = lt[n - 1];
+  if (!isfinite(log_t) || log_t <= lt_first) return XYZA{c[0], c[1], c[2], 1.0};
+  if (log_t >= lt_last) return XYZA{c[3 * (n - 1)], c[3 * (n - 1) + 1], c[3 * (n - 1) + 2], 1.0};
+  const uint32_t idx = lut_index(lt, n, lt_first, lt_last, log_t);
   double lt0 = lt[idx], lt1 = lt[idx + 1];
   const double* c0 = c + 3 * idx;
   const double* c1 = c + 3 * (idx + 1);
@@ -1396,14 +1406,10 @@ GDEV int compute_temperature_lut(const DevObject& o, const double* lut_r, const 
   if (!isfinite(radius)) return GRT_ERR_NON_FINITE_RADIUS;
   if (radius < o.r_isco) return GRT_ERR_BELOW_RISCO;
   uint32_t n = o.lut_n;
-  if (radius <= lut_r[0]) { *out = lut_t[0]; return GRT_OK; }
-  if (radius >= lut_r[n - 1]) { *out = lut_t[n - 1]; return GRT_OK; }
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    uint32_t mid = lo + (hi - lo) / 2;
-    if (lut_r[mid] <= radius) lo = mid + 1; else hi = mid;
-  }
-  uint32_t idx = lo == 0 ? 0 : lo - 1;
+  const double r_first = lut_r[0], r_last = lut_r[n - 1];
+  if (radius <= r_first) { *out = lut_t[0]; return GRT_OK; }
+  if (radius >= r_last) { *out = lut_t[n - 1]; return GRT_OK; }
+  const uint32_t idx = lut_index(lut_r, n, r_first, r_last, radius);
   double r0 = lut_r[idx], t0 = lut_t[idx], r1 = lut_r[idx + 1], t1 = lut_t[idx + 1];
   double t = (radius - r0) / (r1 - r0);
   *out = t0 + t * (t1 - t0);

@@ -126,5 +126,12 @@ hipError_t launch_chunk_live(const unsigned long long* d_count, uint32_t n_chunk
 hipError_t launch_frame_index(const uint32_t* d_sel_local, const unsigned long long* d_count, uint64_t n_max, uint32_t w,
                               uint32_t band_rows, uint32_t shard, uint32_t n_shards, uint32_t* d_sel_frame,
                               hipStream_t stream);
+// Work order of the supersample pass: the first *d_count of d_sel (pixel indices of a
+// w x h rect, n_max entries of room) into d_out, longest expected sub-rays first -- by
+// the 1-spp step counts d_steps (rect order) around each pixel -- ties in selection
+// order.  Call with d_temp == NULL for *temp_bytes (n_max <= INT_MAX).
+hipError_t order_selection(const uint32_t* d_sel, const unsigned long long* d_count, uint64_t n_max,
+                           const uint32_t* d_steps, uint32_t w, uint32_t h, uint32_t* d_out, void* d_temp,
+                           size_t* temp_bytes, hipStream_t stream);
 
 }  // namespace grt

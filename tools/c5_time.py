@@ -1,6 +1,7 @@
 """C5 (BASELINE configs[4]): 1500x1500 schwarzschild.toml with the stock TOML's adaptive
 4x4 supersampling (render_section_to_cie_buffer_supersampled, raytracer.rs:246-458),
 fully on the GPU via grt_render_section.  Prints wall time, selected pixels, steps."""
+import hashlib
 import json
 import sys
 import time
@@ -24,6 +25,7 @@ for k in range(2):
     wall = time.time() - t
     print(json.dumps({"run": k, "wall_s": round(wall, 3), "kernel_ms": st["kernel_ms"], "supersampled_pixels": n_sel,
                       "rays": st["rays"], "accepted_steps": st["accepted_steps"],
+                      "md5": hashlib.md5(out.tobytes()).hexdigest()[:12],
                       "steps_per_s": st["accepted_steps"] / wall,
                       "adaptive": {"samples_per_axis": ad.samples_per_axis,
                                    "luminance_contrast_threshold": ad.luminance_contrast_threshold}}), flush=True)
