@@ -618,7 +618,9 @@ def run_c4(args, rank, world, local_rank, dev):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed frames (default: c2 6, c4 1); the first two frames in flight start together and "
+                    "overlap more than later ones (DESIGN.md section 6), so more frames weigh that start less")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=("c2", "c4"), default="c2")
     ap.add_argument("--size", type=int, default=4096, help="c4: frame edge (4096 = configs[3])")
@@ -637,6 +639,8 @@ def main() -> None:
     ap.add_argument("--self-gather", action="store_true", help="c2, one GPU: run the multi-GPU gather path "
                     "in a process group of one (a check of the streams and RCCL gathers)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 6 if args.workload == "c2" else 1
 
     import torch
     import torch.distributed as dist
