@@ -1809,11 +1809,16 @@ int grt_render_shard_async(grt_scene* s, int device, void* stream, const grt_row
   return enqueue_trace(s, *dc, wl, o, (unsigned long long*)d_stats, (hipStream_t)stream);
 }
 
-int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
-                                 const grt_adaptive_config* cfg, double min_lum, const double* d_min_lum,
-                                 const double* d_frame_ya, const uint8_t* d_frame_class,
-                                 const double* sampling_mask_xyza, double* d_xyza64,
-                                 uint64_t* d_n_supersampled, uint64_t* d_stats, grt_subsample_failures* failures) {
+}  // extern "C"
+
+namespace grt_host {
+// grt_supersample_shard_device; d_local_steps (nullable): the shard's 1-spp step counts in
+// local order, for the sub-rays' longest-first work order (order_selection).
+int supersample_shard(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
+                                const grt_adaptive_config* cfg, double min_lum, const double* d_min_lum,
+                                const double* d_frame_ya, const uint8_t* d_frame_class,
+                                const double* sampling_mask_xyza, double* d_xyza64, const uint32_t* d_local_steps,
+                                uint64_t* d_n_supersampled, uint64_t* d_stats, grt_subsample_failures* failures) {
   if (!s || !cfg || !d_frame_ya || !d_frame_class || !d_xyza64 || !d_stats) return fail(-EINVAL, "null argument");
   if (cfg->samples_per_axis == 0) return fail(-EINVAL, "adaptive_sampling.samples_per_axis must be greater than zero");
   int rc = check_shard(sh);
@@ -1836,12 +1841,15 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
   const uint64_t sub_chunk = g_sub_chunk.load(std::memory_order_relaxed);
   const uint64_t fail_cap = (failures && failures->pixel && failures->status) ? failures->capacity : 0;
   const bool want_events = fail_cap && failures->stop;
-  size_t select_bytes = 0;
+  size_t select_bytes = 0, order_bytes = 0;
   HIP_TRY(grt::compact_flags(nullptr, n_local, nullptr, nullptr, nullptr, &select_bytes, 0));
+  const bool ordered = d_local_steps && !sampling_mask_xyza;
+  if (ordered)
+    HIP_TRY(grt::order_selection(nullptr, nullptr, n_local, nullptr, w, local_rows, nullptr, nullptr, &order_bytes, 0));
   uint8_t* b_flags = nullptr;
-  uint32_t *sel_local = nullptr, *sel_frame = nullptr;
+  uint32_t *sel_local = nullptr, *sel_frame = nullptr, *sel_order = nullptr;
   unsigned long long* d_cnt = nullptr;
-  void* b_select = nullptr;
+  void *b_select = nullptr, *b_order_tmp = nullptr;
   SuperBufs B;
   grt::SubsampleFailures fails{nullptr, nullptr, nullptr, fail_cap};
   auto carve = [&](AdArena& A) {
@@ -1850,6 +1858,10 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
     sel_frame = (uint32_t*)A.take(n_local * 4);
     d_cnt = (unsigned long long*)A.take(16);  // [0] selected pixels, [1] failed sub-samples
     b_select = A.take(select_bytes);
+    if (ordered) {
+      sel_order = (uint32_t*)A.take(n_local * 4);
+      b_order_tmp = A.take(order_bytes);
+    }
     if (!sampling_mask_xyza) B.carve(A, n_local, spa, sub_chunk);
     fails.key = (uint64_t*)A.take(fail_cap * 8);
     fails.status = (uint8_t*)A.take(fail_cap);
@@ -1881,6 +1893,11 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
   // selected pixels in frame order (shard rows increase with local rows): local index
   // for the output, frame index for the jitter hash and the camera ray
   HIP_TRY(grt::compact_flags(b_flags, n_local, sel_local, d_cnt, b_select, &select_bytes, st));
+  if (ordered) {  // longest sub-rays first (the 3 x 3 neighbourhood in the shard's own rows)
+    HIP_TRY(grt::order_selection(sel_local, d_cnt, n_local, d_local_steps, w, local_rows, sel_order, b_order_tmp,
+                                 &order_bytes, st));
+    sel_local = sel_order;
+  }
   HIP_TRY(grt::launch_frame_index(sel_local, d_cnt, n_local, w, sh->band_rows, sh->shard, sh->n_shards, sel_frame,
                                   st));
   if (sampling_mask_xyza) {  // raytracer.rs:285-295: paint instead of supersampling
@@ -1901,6 +1918,19 @@ int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const g
     if ((rc = copy_failures(fails, cnt[1], spa, failures))) return rc;
   }
   return 0;
+}
+
+}  // namespace grt_host
+
+extern "C" {
+
+int grt_supersample_shard_device(grt_scene* s, int device, void* stream, const grt_row_shard* sh,
+                                 const grt_adaptive_config* cfg, double min_lum, const double* d_min_lum,
+                                 const double* d_frame_ya, const uint8_t* d_frame_class,
+                                 const double* sampling_mask_xyza, double* d_xyza64,
+                                 uint64_t* d_n_supersampled, uint64_t* d_stats, grt_subsample_failures* failures) {
+  return grt_host::supersample_shard(s, device, stream, sh, cfg, min_lum, d_min_lum, d_frame_ya, d_frame_class,
+                                     sampling_mask_xyza, d_xyza64, nullptr, d_n_supersampled, d_stats, failures);
 }
 
 int grt_supersample_shard(grt_scene* s, int device, void* stream, const grt_row_shard* sh,

@@ -256,6 +256,7 @@ struct DevBufs {
   uint8_t* block = nullptr;             // send block (fields of plan.mask)
   float* x32 = nullptr;                 // f32 XYZA when the plan does not send it
   double* x64 = nullptr;                // f64 XYZA when the plan does not send it (supersampling sends it)
+  uint32_t* steps = nullptr;            // 1-spp step counts when supersampling and the plan does not send them
   uint8_t *ag_send = nullptr, *ag_recv = nullptr;
   double* frame_ya = nullptr;
   uint8_t* frame_cls = nullptr;
@@ -270,6 +271,7 @@ void carve(Carve& A, const Plan& P, int i, DevBufs& B) {
   B.block = (uint8_t*)A.take(P.block[i]);
   if (!(P.mask & (1u << grt::RF_XYZA32))) B.x32 = (float*)A.take(n * 16);
   if (P.super) {
+    if (!(P.mask & (1u << grt::RF_STEPS))) B.steps = (uint32_t*)A.take(n * 4);
     B.ag_send = (uint8_t*)A.take(P.ag_bytes);
     B.ag_recv = (uint8_t*)A.take(P.ag_bytes * P.n_dev);
     B.frame_ya = (double*)A.take(F * 16);
@@ -351,7 +353,9 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
     double* x64 = (double*)field_ptr(B.block, P.mask, n, grt::RF_XYZA64);
     uint8_t* cls = field_ptr(B.block, P.mask, n, grt::RF_CLASS);
     uint8_t* status = field_ptr(B.block, P.mask, n, grt::RF_STATUS);
-    uint32_t* steps = (uint32_t*)field_ptr(B.block, P.mask, n, grt::RF_STEPS);
+    // the supersample pass orders its sub-rays by the 1-spp step counts: traced always then
+    uint32_t* steps = (P.mask & (1u << grt::RF_STEPS)) ? (uint32_t*)field_ptr(B.block, P.mask, n, grt::RF_STEPS)
+                                                       : B.steps;
     uint8_t* stop = field_ptr(B.block, P.mask, n, grt::RF_STOP);
     if (n) {
       int rc = grt_render_shard_async(scene, dev, st, &sh, x32, cls, status, x64, steps, stop, (uint64_t*)B.stats);
@@ -389,7 +393,7 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
       if (int rc = launch_deinterleave(L, B.ag_recv, d, st)) return rc;
       HIP_TRY(hipEventRecord(M.ev[3], st));
       // the frame's exact 99th-percentile floor (or the configured minimum), then this
-      // device's selection and sub-rays (grt_supersample_shard_device)
+      // device's selection and sub-rays (grt_supersample_shard_device, longest first)
       const bool dev_floor = !cfg->has_minimum_luminance;
       if (dev_floor) {
         int rc = grt_adaptive_floor_device(scene, dev, st, B.frame_ya, 2, L.n_pixels, B.floor);
@@ -414,9 +418,9 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
         }
         flp = &fl;
       }
-      int rc = grt_supersample_shard_device(scene, dev, st, &sh, cfg, cfg->minimum_luminance,
-                                            dev_floor ? B.floor : nullptr, B.frame_ya, B.frame_cls, mask_xyza, x64,
-                                            (uint64_t*)(B.stats + 4), (uint64_t*)B.stats, flp);
+      int rc = grt_host::supersample_shard(scene, dev, st, &sh, cfg, cfg->minimum_luminance,
+                                           dev_floor ? B.floor : nullptr, B.frame_ya, B.frame_cls, mask_xyza, x64,
+                                           steps, (uint64_t*)(B.stats + 4), (uint64_t*)B.stats, flp);
       if (rc) return rc;
       R.f_count = flp ? fl.count : 0;
     }

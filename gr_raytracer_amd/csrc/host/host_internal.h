@@ -34,6 +34,12 @@ void parallel_for(uint64_t n, F&& fn) {
 }
 // The camera frame of a device scene (grt_scene_desc.camera rows x cols; api.hip).
 void scene_frame_size(const grt_scene* s, int64_t* rows, int64_t* cols);
+// grt_supersample_shard_device with the shard's 1-spp step counts (d_local_steps, local
+// order, nullable) for the sub-rays' longest-first work order (api.hip).
+int supersample_shard(grt_scene* s, int device, void* stream, const grt_row_shard* sh, const grt_adaptive_config* cfg,
+                      double min_lum, const double* d_min_lum, const double* d_frame_ya, const uint8_t* d_frame_class,
+                      const double* sampling_mask_xyza, double* d_xyza64, const uint32_t* d_local_steps,
+                      uint64_t* d_n_supersampled, uint64_t* d_stats, grt_subsample_failures* failures);
 double rclamp_pub(double v, double lo, double hi);
 int camera_build(int geometry, double radius, double a, const double position[4], const double velocity[4],
                  double alpha, int64_t rows, int64_t cols, double phi, double theta, double psi,
