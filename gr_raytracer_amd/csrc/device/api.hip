@@ -73,7 +73,9 @@ struct DeviceCopy {
   std::vector<void*> allocations;
   unsigned long long* d_counter = nullptr;  // [0] work counter, [5..6] hit pool (HitPool::count)
   unsigned long long* d_stats = nullptr;    // [0..3] accepted, attempts, rays, overflows
-  unsigned long long* d_march = nullptr;    // [0] jobs, [1] job cursor, [2] samples, [3] jobs (cumulative)
+  // [0] jobs, [1] job cursor, [2] samples, [3] jobs (cumulative), [4] noise samples,
+  // [5] emitting samples, [8 + k] march_kernel's claim cursor of object k's pass
+  unsigned long long* d_march = nullptr;
   bool vol = false;                         // the scene has VolumetricDiscs
   int cus = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -485,9 +487,9 @@ int init_device_copy(grt_scene* s, int device, DeviceCopy& dc) {
   if ((rc = upload(dc, &ds, 1, &dsp))) return rc;
   dc.d_scene = dsp;
   void* p = nullptr;
-  HIP_TRY(hipMalloc(&p, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&p, (16 + 8 + GRT_MAX_OBJECTS) * sizeof(unsigned long long)));
   dc.allocations.push_back(p);
-  HIP_TRY(hipMemset(p, 0, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(p, 0, (16 + 8 + GRT_MAX_OBJECTS) * sizeof(unsigned long long)));
   dc.d_counter = (unsigned long long*)p;
   dc.d_stats = dc.d_counter + 1;
   dc.d_march = dc.d_counter + 8;
@@ -674,7 +676,10 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
     wl.two_ended = (k.two_ended != 0 && wl.n_items < (1ull << 31)) ? 1u : 0u;
   }
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
-  if (dc.vol) HIP_TRY(hipMemsetAsync(dc.d_march, 0, 2 * sizeof(unsigned long long), stream));  // jobs, cursor
+  if (dc.vol) {  // jobs, cursor; the march passes' cursors
+    HIP_TRY(hipMemsetAsync(dc.d_march, 0, 2 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(dc.d_march + 8, 0, GRT_MAX_OBJECTS * sizeof(unsigned long long), stream));
+  }
   int threads = k.threads ? k.threads : 256;
   int blocks = k.blocks_per_cu > 0 ? dc.cus * k.blocks_per_cu
                                    : dc.cus * 2 * grt::integrate_waves(s->desc.geometry, dc.vol);
@@ -711,9 +716,11 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
   // grt_set_arithmetic(1): the light charts' kernels built with FMA contraction
   // (geodesic_fused.hip); Kerr-Schild always runs the exact ones
   const bool fused = k.arith == 1 && s->desc.geometry != GRT_GEOM_KERR;
-  HIP_TRY((fused ? grt::fused::launch_trace : grt::launch_trace)(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter,
-                                                                  d_stats, blocks, threads, dc.vol, tl, tail_blocks,
-                                                                  stream));
+  const auto launch = fused ? grt::fused::launch_trace
+                            : (s->desc.geometry == GRT_GEOM_KERR_BL ? grt::kerr_bl::launch_trace : grt::launch_trace);
+  // the exact KerrBL kernels are a unit of their own (geodesic_kerr_bl.hip)
+  HIP_TRY(launch(s->desc.geometry, dc.d_scene, wl, ws, o, dc.d_counter, d_stats, blocks, threads, dc.vol, tl,
+                 tail_blocks, stream));
   return stream_done(dc, stream);
 }
 

@@ -39,10 +39,19 @@
 #ifndef GRT_FUSED
 #define GRT_FUSED 0
 #endif
+// GRT_KERR_BL_TU: this file compiled a second time, by geodesic_kerr_bl.hip, without the
+// machine-level loop-invariant code motion, into namespace grt::kerr_bl: the KerrBL trace
+// kernels (launch_trace for GRT_GEOM_KERR_BL only; the exact build leaves them out).
+#ifndef GRT_KERR_BL_TU
+#define GRT_KERR_BL_TU 0
+#endif
+#define GRT_MAIN_TU (!GRT_FUSED && !GRT_KERR_BL_TU)
 
 namespace grt {
 #if GRT_FUSED
 namespace fused {
+#elif GRT_KERR_BL_TU
+namespace kerr_bl {
 #endif
 
 #ifndef GDEV
@@ -246,7 +255,7 @@ GDEV double ksqrt(double x) {
   else return sqrt(x);
 }
 
-#if !GRT_FUSED
+#if GRT_MAIN_TU
 // Device check of div_inrange / div2_inrange / div_fx / sqrt_fx against the compiler's
 // division and sqrt over the whole exponent plane (tests/test_gpu_parity.py
 // ::test_range_free_arithmetic_map): thread (ex, ey), ex, ey biased exponents 0 .. 2046
@@ -301,7 +310,7 @@ __global__ void arith_map_kernel(uint32_t samples, uint64_t seed, uint8_t* map, 
   if (ex == 0) zmap[ey] = (uint8_t)zflags;
   if (ey == 0) smap[ex] = (uint8_t)sflags;
 }
-#endif  // !GRT_FUSED
+#endif  // GRT_MAIN_TU
 
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 2.0 * 3.14159265358979323846;
@@ -1785,8 +1794,23 @@ GDEV unsigned long long hw_place() {
   const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
   return ((unsigned long long)xcc << 32) | hw;
 }
-#if !GRT_FUSED
+#if GRT_MAIN_TU  // the KerrBL unit's kernels record too
+hipError_t set_ray_times(unsigned long long* p) {
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_ray_times), &p, sizeof(p));
+  return e != hipSuccess ? e : kerr_bl::set_ray_times(p);
+}
+#elif GRT_KERR_BL_TU
 hipError_t set_ray_times(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_ray_times), &p, sizeof(p)); }
+#endif
+#if GRT_KERR_BL_TU && GRT_PATH_COUNT
+hipError_t path_read(unsigned long long* out, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_path), sizeof(g_path));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[2 * NPATH] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_path), z, sizeof(z));
+  }
+  return e;
+}
 #endif
 #define RAY_TIME(n, idx, k, v) ray_time(n, idx, k, v)
 #else
@@ -2449,7 +2473,7 @@ __global__ void __launch_bounds__(256, GRT_TAIL_WAVES) tail_kernel(const DevScen
   }
 }
 
-#if !GRT_FUSED  // trajectories, monitors, probes and test hooks: exact build only
+#if GRT_MAIN_TU  // trajectories, monitors, probes and test hooks: exact build only
 // ======================================================= trajectory kernel =======
 // Integrator::integrate with the whole Vec<Step> kept (integrator.rs:78-174), the path
 // of `render-ray` / `render-ray-at` (main.rs:117-171, ray.rs:35-54).  One lane per ray;
@@ -2577,12 +2601,16 @@ hipError_t launch_rhs_check(int geometry, const DevScene* d_scene, const double*
 }
 
 #if GRT_PATH_COUNT
+// this unit's counters plus the KerrBL unit's
 hipError_t path_read(unsigned long long* out, bool reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_path), sizeof(g_path));
   if (e == hipSuccess && reset) {
     const unsigned long long z[2 * NPATH] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_path), z, sizeof(z));
   }
+  unsigned long long bl[2 * NPATH];
+  if (e == hipSuccess) e = kerr_bl::path_read(bl, reset);
+  for (int k = 0; e == hipSuccess && k < 2 * NPATH; ++k) out[k] += bl[k];
   return e;
 }
 #endif
@@ -2949,7 +2977,7 @@ hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& w
 }
 
 
-#endif  // !GRT_FUSED
+#endif  // GRT_MAIN_TU
 // ============================================================ shade kernel =======
 // Evaluate one recorded candidate: the emitter step at the intersection
 // (objects.rs:27-44 + :95-115), its redshift, temperature and texture colour.
@@ -3331,29 +3359,35 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
                         int threads, bool vol, const TailList& tl, int tail_blocks, hipStream_t stream) {
   if (ws.n == 0) return hipSuccess;
   switch (geometry) {
+#if !GRT_KERR_BL_TU
     case GRT_GEOM_EUCLIDEAN:
       return launch_g<GRT_GEOM_EUCLIDEAN>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
                                           tail_blocks, stream);
     case GRT_GEOM_SCHWARZSCHILD:
       return launch_g<GRT_GEOM_SCHWARZSCHILD>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
                                               tail_blocks, stream);
-#if !GRT_FUSED  // Kerr-Schild always runs exact (grt_set_arithmetic)
+#endif
+#if GRT_MAIN_TU  // Kerr-Schild always runs exact (grt_set_arithmetic)
     case GRT_GEOM_KERR:
       return launch_g<GRT_GEOM_KERR>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl, tail_blocks,
                                      stream);
 #endif
+#if !GRT_MAIN_TU  // the exact KerrBL trace is grt::kerr_bl's
     case GRT_GEOM_KERR_BL:
       return launch_g<GRT_GEOM_KERR_BL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol, tl,
                                         tail_blocks, stream);
+#endif
+#if !GRT_KERR_BL_TU
     case GRT_GEOM_EUCLIDEAN_SPHERICAL:
       return launch_g<GRT_GEOM_EUCLIDEAN_SPHERICAL>(d_scene, wl, ws, out, d_counter, d_stats, blocks, threads, vol,
                                                     tl, tail_blocks, stream);
+#endif
     default:
       return hipErrorInvalidValue;
   }
 }
 
-#if GRT_FUSED
-}  // namespace fused
+#if GRT_FUSED || GRT_KERR_BL_TU
+}  // namespace fused / kerr_bl
 #endif
 }  // namespace grt

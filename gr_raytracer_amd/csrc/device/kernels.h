@@ -63,6 +63,19 @@ hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& w
                         int blocks, int threads, bool vol, const TailList& tl, int tail_blocks,
                         hipStream_t stream);
 }  // namespace fused
+// The exact KerrBL trace (geodesic_kerr_bl.hip: the same code compiled without machine
+// loop-invariant code motion, which hoisted ~100 VGPRs of polynomial constants out of the
+// loops and made the 3-wave integrate kernel spill; C3 -2%, its raymarch -7%, profiles/r06p).
+namespace kerr_bl {
+hipError_t launch_trace(int geometry, const DevScene* d_scene, const WorkList& wl, const Workspace& ws,
+                        const Outputs& out, unsigned long long* d_counter, unsigned long long* d_stats,
+                        int blocks, int threads, bool vol, const TailList& tl, int tail_blocks,
+                        hipStream_t stream);
+hipError_t set_ray_times(unsigned long long* p);
+#if GRT_PATH_COUNT
+hipError_t path_read(unsigned long long* out, bool reset);
+#endif
+}  // namespace kerr_bl
 hipError_t launch_trajectories(int geometry, const DevScene* d_scene, const TrajectoryList& tl, hipStream_t stream);
 
 // Invariant monitors of the n = rows x cols rays of a rectangle (health_kernel):

@@ -334,7 +334,7 @@ GDEV bool vdisc_no_more_density(const DevObject& o, const V3& p, const V3& rd) {
 // Job = (ray slot << 8) | candidate slot, colour to ws.vcol at the candidate slot; or
 // JOB_POOL | ray << 31 | pool record, colour to the record's vcol.
 // The per-sample table lookups (temperature LUT of the first volumetric object with one,
-// the blackbody LUT) are binary searches of ~10 dependent loads: staged in LDS (48 KB).
+// the blackbody LUT; lut_index) are staged in LDS (48 KB).
 constexpr uint32_t MARCH_LUT_MAX = 1000;
 template <int G>
 __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restrict__ Sp, Workspace ws) {
@@ -372,150 +372,164 @@ __global__ void __launch_bounds__(256, 2) march_kernel(const DevScene* __restric
   const uint64_t n = ws.n;
   const uint64_t MN = (uint64_t)GRT_WS_SLOTS * n;
   constexpr uint64_t CHUNK = 64;
-  uint64_t chunk_next = 0, chunk_end = 0;
-  bool active = false, done = false;
-  // lane state
-  uint64_t slot = 0, i = 0, n_samples = 0, n_noise = 0, n_emit = 0;
-  uint32_t k = 0;
-  V3 ro{0, 0, 0}, rd{0, 0, 0};
-  double d_o = 0.0, exit_d = 0.0, transparency = 1.0, aws = 0.0, awt = 0.0;
-  double acc_x = 0.0, acc_y = 0.0, acc_z = 0.0, obs = 0.0, f_pt = 0.0, f_pphi = 0.0;
-  bool cached = false, pool_job = false;
-
-  while (true) {
-    bool need = !active && !done;
-    uint64_t need_mask = __ballot(need);
-    if (need_mask) {
-      uint64_t cnt = __popcll(need_mask);
-      uint64_t remaining = chunk_end - chunk_next;
-      uint64_t new_base = 0;
-      if (cnt > remaining) {
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(ws.march + 1, (unsigned long long)CHUNK);
-        new_base = __shfl(b, 0);
-      }
-      if (need) {
-        uint64_t rank = __popcll(need_mask & lanemask_lt);
-        uint64_t item = rank < remaining ? chunk_next + rank : new_base + (rank - remaining);
-        if (item >= n_jobs) {
-          done = true;
-        } else {
-          const uint64_t job = ws.jobs[item];
-          pool_job = (job & JOB_POOL) != 0;
-          uint64_t idx;
-          V3 dir;
-          if (!pool_job) {
-            idx = job >> 8;
-            const uint32_t j = (uint32_t)(job & 255u);
-            slot = (uint64_t)j * n + idx;
-            k = ws.rec[slot].obj;
-            ro = V3{ws.rec[slot].pt[0], ws.rec[slot].pt[1], ws.rec[slot].pt[2]};
-            dir = V3{ws.rec_dir[slot], ws.rec_dir[MN + slot], ws.rec_dir[2 * MN + slot]};
-          } else {  // a candidate past the workspace slots (HitPool record)
-            idx = (job & ~JOB_POOL) >> 31;
-            slot = job & 0x7fffffffull;
-            const uint64_t m = ws.pool->cap;
-            k = ws.pool->obj[slot];
-            ro = V3{ws.pool->pt[slot], ws.pool->pt[m + slot], ws.pool->pt[2 * m + slot]};
-            dir = V3{ws.pool->dir[slot], ws.pool->dir[m + slot], ws.pool->dir[2 * m + slot]};
-          }
-          const double dn = vnorm(dir);  // .normalize()
-          rd = V3{dir.x / dn, dir.y / dn, dir.z / dn};
-          obs = ws.rc[idx];
-          f_pt = ws.rc[4 * n + idx];
-          f_pphi = ws.rc[5 * n + idx];
-          cached = vdisc_exit_distance(S.obj[k], ro, rd, &exit_d);
-          d_o = 0.0;
-          i = 0;
-          transparency = 1.0;
-          aws = awt = 0.0;
-          acc_x = acc_y = acc_z = 0.0;
-          active = true;
-        }
-      }
-      if (cnt > remaining) {
-        chunk_next = new_base + (cnt - remaining);
-        chunk_end = new_base + CHUNK;
-      } else {
-        chunk_next += cnt;
-      }
-    }
-    if (__ballot(!done) == 0) break;
-    if (!active) continue;
-
-    // ---- one sample (raymarch_constant_step_internal, :234-309) ----
-    const DevObject& o = S.obj[k];
+  uint64_t n_samples = 0, n_noise = 0, n_emit = 0;
+  // One pass over the job list per VolumetricDisc of the scene, each with its own claim
+  // cursor (ws.march[8 + kobj]): a pass marches only its object's jobs, so the object is
+  // wave-uniform and its parameters sit in scalar registers (per-lane object loads held
+  // ~80 VGPRs across the sample loop).  The stock scenes have one such object: one pass.
+  for (uint32_t kobj = 0; kobj < S.n_objects; ++kobj) {
+    if (S.obj[kobj].kind != GRT_OBJ_VOLUMETRIC_DISC) continue;
+    const DevObject& o = S.obj[kobj];
     const uint8_t* P = lds_perm + o.perm_slot * 256u;
-    const double d_s = o.m_step;
-    const V3 p{ro.x + rd.x * d_o, ro.y + rd.y * d_o, ro.z + rd.z * d_o};
-    d_o += d_s;
-    n_samples++;
-    bool failed = false;
-    PlaneAngle pa;
-    bool noise;
-    const double density = vdisc_density(o, P, lds_grad, p, &pa, &noise);
-    n_noise += noise ? 1u : 0u;
-    if (density > 0.0) {
-      const double sig = o.sig_a + o.sig_s;
-      transparency *= glibc::exp_(-d_s * density * sig);
-      double ut, uphi;
-      if (killing_at<G>(S, p, &ut, &uphi)) {
-        const double emitter_energy = ut * f_pt + uphi * f_pphi;
-        const double redshift = obs / emitter_energy;
-        const double r_dist = vnorm(vcross(p, vaxis(o)));
-        double temperature;
-        const bool lds_t = (int)k == lut_obj;
-        if (compute_temperature_lut(o, lds_t ? lds_tr : o.lut_r, lds_t ? lds_tt : o.lut_t, r_dist, &temperature) !=
-            GRT_OK) {
-          failed = true;  // Err -> color_at_uv's unwrap_or_else: (0, 0, 0, 0)
+    const bool lds_t = (int)kobj == lut_obj;
+    const double* lut_r = lds_t ? lds_tr : o.lut_r;
+    const double* lut_t = lds_t ? lds_tt : o.lut_t;
+    unsigned long long* cursor = ws.march + 8 + kobj;
+    uint64_t chunk_next = 0, chunk_end = 0;
+    bool active = false, done = false;
+    // lane state
+    uint64_t slot = 0, i = 0;
+    V3 ro{0, 0, 0}, rd{0, 0, 0};
+    double d_o = 0.0, exit_d = 0.0, transparency = 1.0, aws = 0.0, awt = 0.0;
+    double acc_x = 0.0, acc_y = 0.0, acc_z = 0.0, obs = 0.0, f_pt = 0.0, f_pphi = 0.0;
+    bool cached = false, pool_job = false;
+
+    while (true) {
+      bool need = !active && !done;
+      uint64_t need_mask = __ballot(need);
+      if (need_mask) {
+        uint64_t cnt = __popcll(need_mask);
+        uint64_t remaining = chunk_end - chunk_next;
+        uint64_t new_base = 0;
+        if (cnt > remaining) {
+          unsigned long long b = 0;
+          if (lane == 0) b = atomicAdd(cursor, (unsigned long long)CHUNK);
+          new_base = __shfl(b, 0);
+        }
+        if (need) {
+          uint64_t rank = __popcll(need_mask & lanemask_lt);
+          uint64_t item = rank < remaining ? chunk_next + rank : new_base + (rank - remaining);
+          if (item >= n_jobs) {
+            done = true;
+          } else {
+            const uint64_t job = ws.jobs[item];
+            pool_job = (job & JOB_POOL) != 0;
+            uint64_t idx;
+            uint32_t k;
+            if (!pool_job) {
+              idx = job >> 8;
+              slot = (uint64_t)(uint32_t)(job & 255u) * n + idx;
+              k = ws.rec[slot].obj;
+            } else {  // a candidate past the workspace slots (HitPool record)
+              idx = (job & ~JOB_POOL) >> 31;
+              slot = job & 0x7fffffffull;
+              k = ws.pool->obj[slot];
+            }
+            if (k == kobj) {  // another object's job waits for that object's pass
+              V3 dir;
+              if (!pool_job) {
+                ro = V3{ws.rec[slot].pt[0], ws.rec[slot].pt[1], ws.rec[slot].pt[2]};
+                dir = V3{ws.rec_dir[slot], ws.rec_dir[MN + slot], ws.rec_dir[2 * MN + slot]};
+              } else {
+                const uint64_t m = ws.pool->cap;
+                ro = V3{ws.pool->pt[slot], ws.pool->pt[m + slot], ws.pool->pt[2 * m + slot]};
+                dir = V3{ws.pool->dir[slot], ws.pool->dir[m + slot], ws.pool->dir[2 * m + slot]};
+              }
+              const double dn = vnorm(dir);  // .normalize()
+              rd = V3{dir.x / dn, dir.y / dn, dir.z / dn};
+              obs = ws.rc[idx];
+              f_pt = ws.rc[4 * n + idx];
+              f_pphi = ws.rc[5 * n + idx];
+              cached = vdisc_exit_distance(o, ro, rd, &exit_d);
+              d_o = 0.0;
+              i = 0;
+              transparency = 1.0;
+              aws = awt = 0.0;
+              acc_x = acc_y = acc_z = 0.0;
+              active = true;
+            }
+          }
+        }
+        if (cnt > remaining) {
+          chunk_next = new_base + (cnt - remaining);
+          chunk_end = new_base + CHUNK;
         } else {
-          n_emit++;
-          double u, v;
-          vdisc_uv(o, pa, &u, &v);
-          const XYZA light = texture_color_lut(S, o.tex, u, v, redshift, temperature, bb_lt, bb_xyz);
-          const double light_attenuation = glibc::exp_(-density * d_s * sig);
-          const double ratio = temperature / o.bref;
-          const double r2 = ratio * ratio;
-          const double intensity = r2 * r2;  // powi(4)
-          const double emission_weight = transparency * light_attenuation * o.sig_s * density * d_s;
-          const double w = emission_weight * intensity;
-          const double asw = density * d_s;
-          aws += rclamp(light.a, 0.0, 1.0) * asw;
-          awt += asw;
-          acc_x += light.x * w;
-          acc_y += light.y * w;
-          acc_z += light.z * w;
+          chunk_next += cnt;
         }
       }
-    }
-    bool finished = failed || (density == 0.0 && vdisc_no_more_density(o, p, rd));
-    if (!finished) {
-      bool exited;
-      if (cached) {
-        exited = d_o >= exit_d;
-      } else {  // does_exit (:154-170): a crossing within this step
-        const double st[3] = {p.x, p.y, p.z};
-        const double end[3] = {p.x + rd.x * d_s, p.y + rd.y * d_s, p.z + rd.z * d_s};
-        double tx, ipx[3];
-        exited = vdisc_chord(o, st, end, &tx, ipx) && tx > 1e-9;
+      if (__ballot(!done) == 0) break;
+      if (!active) continue;
+
+      // ---- one sample (raymarch_constant_step_internal, :234-309) ----
+      const double d_s = o.m_step;
+      const V3 p{ro.x + rd.x * d_o, ro.y + rd.y * d_o, ro.z + rd.z * d_o};
+      d_o += d_s;
+      n_samples++;
+      bool failed = false;
+      PlaneAngle pa;
+      bool noise;
+      const double density = vdisc_density(o, P, lds_grad, p, &pa, &noise);
+      n_noise += noise ? 1u : 0u;
+      if (density > 0.0) {
+        const double sig = o.sig_a + o.sig_s;
+        transparency *= glibc::exp_(-d_s * density * sig);
+        double ut, uphi;
+        if (killing_at<G>(S, p, &ut, &uphi)) {
+          const double emitter_energy = ut * f_pt + uphi * f_pphi;
+          const double redshift = obs / emitter_energy;
+          const double r_dist = vnorm(vcross(p, vaxis(o)));
+          double temperature;
+          if (compute_temperature_lut(o, lut_r, lut_t, r_dist, &temperature) != GRT_OK) {
+            failed = true;  // Err -> color_at_uv's unwrap_or_else: (0, 0, 0, 0)
+          } else {
+            n_emit++;
+            double u, v;
+            vdisc_uv(o, pa, &u, &v);
+            const XYZA light = texture_color_lut(S, o.tex, u, v, redshift, temperature, bb_lt, bb_xyz);
+            const double light_attenuation = glibc::exp_(-density * d_s * sig);
+            const double ratio = temperature / o.bref;
+            const double r2 = ratio * ratio;
+            const double intensity = r2 * r2;  // powi(4)
+            const double emission_weight = transparency * light_attenuation * o.sig_s * density * d_s;
+            const double w = emission_weight * intensity;
+            const double asw = density * d_s;
+            aws += rclamp(light.a, 0.0, 1.0) * asw;
+            awt += asw;
+            acc_x += light.x * w;
+            acc_y += light.y * w;
+            acc_z += light.z * w;
+          }
+        }
       }
-      finished = exited || ++i >= o.m_max;
-    }
-    if (finished) {
-      double col[4] = {0.0, 0.0, 0.0, 0.0};
-      if (!failed) {
-        const double physical_opacity = 1.0 - transparency;
-        const double texture_alpha = awt > 0.0 ? aws / awt : 1.0;
-        col[0] = acc_x;
-        col[1] = acc_y;
-        col[2] = acc_z;
-        col[3] = physical_opacity * texture_alpha;
+      bool finished = failed || (density == 0.0 && vdisc_no_more_density(o, p, rd));
+      if (!finished) {
+        bool exited;
+        if (cached) {
+          exited = d_o >= exit_d;
+        } else {  // does_exit (:154-170): a crossing within this step
+          const double st[3] = {p.x, p.y, p.z};
+          const double end[3] = {p.x + rd.x * d_s, p.y + rd.y * d_s, p.z + rd.z * d_s};
+          double tx, ipx[3];
+          exited = vdisc_chord(o, st, end, &tx, ipx) && tx > 1e-9;
+        }
+        finished = exited || ++i >= o.m_max;
       }
-      double* vc = pool_job ? ws.pool->vcol : ws.vcol;
-      const uint64_t m = pool_job ? ws.pool->cap : MN;
+      if (finished) {
+        double col[4] = {0.0, 0.0, 0.0, 0.0};
+        if (!failed) {
+          const double physical_opacity = 1.0 - transparency;
+          const double texture_alpha = awt > 0.0 ? aws / awt : 1.0;
+          col[0] = acc_x;
+          col[1] = acc_y;
+          col[2] = acc_z;
+          col[3] = physical_opacity * texture_alpha;
+        }
+        double* vc = pool_job ? ws.pool->vcol : ws.vcol;
+        const uint64_t m = pool_job ? ws.pool->cap : MN;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) vc[q * m + slot] = col[q];
-      active = false;
+        for (int q = 0; q < 4; ++q) vc[q * m + slot] = col[q];
+        active = false;
+      }
     }
   }
 #pragma unroll
