@@ -374,6 +374,32 @@ def _mask_pc_relative(code: bytearray) -> None:
             code[i + 16:i + 20] = bytes(4)
 
 
+def _gfx950_code_objects(data: bytes, path) -> list:
+    """Offsets of the gfx950 code objects in the `.hip_fatbin` section: one offload bundle
+    per translation unit with device code, back to back."""
+    import struct
+
+    fb_off, fb_size, _, _ = _elf_sections(data)[".hip_fatbin"]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    if data[fb_off:fb_off + len(magic)] != magic:
+        raise GrtError(f"{path}: .hip_fatbin is not an uncompressed offload bundle")
+    out = []
+    b = fb_off
+    while b >= 0 and b < fb_off + fb_size:
+        p = b + len(magic)
+        n, = struct.unpack_from("<Q", data, p)
+        p += 8
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            if "gfx950" in data[p + 24:p + 24 + tlen].decode():
+                out.append(b + off)
+            p += 24 + tlen
+        b = data.find(magic, p, fb_off + fb_size)
+    if not out:
+        raise GrtError(f"{path}: no gfx950 code object in the bundle")
+    return out
+
+
 def kernel_code_sha256(symbol: str, path: Path = LIB_PATH) -> str:
     """SHA-256 of ONE kernel's gfx950 machine code and kernel descriptor inside
     libgrt.so: the bytes of the function symbol `symbol` (mangled name) and of
@@ -385,22 +411,17 @@ def kernel_code_sha256(symbol: str, path: Path = LIB_PATH) -> str:
     import struct
 
     data = Path(path).read_bytes()
-    fb_off, fb_size, _, _ = _elf_sections(data)[".hip_fatbin"]
-    magic = b"__CLANG_OFFLOAD_BUNDLE__"
-    if data[fb_off:fb_off + len(magic)] != magic:
-        raise GrtError(f"{path}: .hip_fatbin is not an uncompressed offload bundle")
-    p = fb_off + len(magic)
-    n, = struct.unpack_from("<Q", data, p)
-    p += 8
     co = None
-    for _ in range(n):
-        off, size, tlen = struct.unpack_from("<QQQ", data, p)
-        triple = data[p + 24:p + 24 + tlen].decode()
-        p += 24 + tlen
-        if "gfx950" in triple:
-            co = fb_off + off
+    for c in _gfx950_code_objects(data, path):  # the code object that defines the kernel
+        sym_off, sym_size, str_off, entsize = _elf_sections(data, c)[".symtab"]
+        names = {data[str_off + struct.unpack_from("<I", data, sym_off + k * entsize)[0]:
+                      data.index(b"\0", str_off + struct.unpack_from("<I", data, sym_off + k * entsize)[0])].decode()
+                 for k in range(sym_size // entsize)}
+        if symbol in names:
+            co = c
+            break
     if co is None:
-        raise GrtError(f"{path}: no gfx950 code object in the bundle")
+        raise GrtError(f"{path}: kernel symbol {symbol} not found")
     secs = _elf_sections(data, co)
     sym_off, sym_size, str_off, entsize = secs[".symtab"]
     h = hashlib.sha256()
@@ -431,41 +452,32 @@ def kernel_code_sha256(symbol: str, path: Path = LIB_PATH) -> str:
 
 
 def kernel_symbols(path: Path = LIB_PATH) -> list:
-    """Mangled names of the kernels in libgrt.so's gfx950 code object."""
+    """Mangled names of the kernels in libgrt.so's gfx950 code objects (every unit)."""
     import struct
 
     data = Path(path).read_bytes()
-    fb_off, _, _, _ = _elf_sections(data)[".hip_fatbin"]
-    p = fb_off + 24
-    n, = struct.unpack_from("<Q", data, p)
-    p += 8
-    co = None
-    for _ in range(n):
-        off, size, tlen = struct.unpack_from("<QQQ", data, p)
-        if "gfx950" in data[p + 24:p + 24 + tlen].decode():
-            co = fb_off + off
-        p += 24 + tlen
-    sym_off, sym_size, str_off, entsize = _elf_sections(data, co)[".symtab"]
     out = []
-    for k in range(sym_size // entsize):
-        st_name, = struct.unpack_from("<I", data, sym_off + k * entsize)
-        nm = data[str_off + st_name:data.index(b"\0", str_off + st_name)].decode()
-        if nm.endswith(".kd"):
-            out.append(nm[:-3])
+    for co in _gfx950_code_objects(data, path):
+        sym_off, sym_size, str_off, entsize = _elf_sections(data, co)[".symtab"]
+        for k in range(sym_size // entsize):
+            st_name, = struct.unpack_from("<I", data, sym_off + k * entsize)
+            nm = data[str_off + st_name:data.index(b"\0", str_off + st_name)].decode()
+            if nm.endswith(".kd"):
+                out.append(nm[:-3])
     return out
 
 
 def kernel_symbol(demangled: str, path: Path = LIB_PATH) -> str:
-    """Mangled name of a `grt::name<int-or-bool, ...>` kernel, e.g.
-    "grt::integrate_kernel<1, false>" -> "_ZN3grt16integrate_kernelILi1ELb0EE..."."""
+    """Mangled name of a `grt::name<int-or-bool, ...>` (or `grt::ns::name<...>`) kernel,
+    e.g. "grt::integrate_kernel<1, false>" -> "_ZN3grt16integrate_kernelILi1ELb0EE..."."""
     import re
 
-    m = re.fullmatch(r"grt::(\w+)<([^>]*)>", demangled.strip())
+    m = re.fullmatch(r"grt::(?:(\w+)::)?(\w+)<([^>]*)>", demangled.strip())
     if not m:
         raise GrtError(f"cannot mangle {demangled!r}")
-    name, args = m.group(1), [a.strip() for a in m.group(2).split(",")]
+    ns, name, args = m.group(1), m.group(2), [a.strip() for a in m.group(3).split(",")]
     enc = "".join("Lb1E" if a == "true" else "Lb0E" if a == "false" else f"Li{int(a)}E" for a in args)
-    prefix = f"_ZN3grt{len(name)}{name}I{enc}E"
+    prefix = f"_ZN3grt{len(ns)}{ns}{len(name)}{name}I{enc}E" if ns else f"_ZN3grt{len(name)}{name}I{enc}E"
     hits = [k for k in kernel_symbols(path) if k.startswith(prefix)]
     if len(hits) != 1:
         raise GrtError(f"{demangled}: {len(hits)} matching kernel symbols")
