@@ -409,15 +409,25 @@ int main(int argc, char** argv) {
     filename = action == "render" ? "render.png" : (action == "render-ray" ? "rendered-ray.csv" : "rendered-ray-at.csv");
   if (config_file.empty()) return usage("Config file is required for this action");
 
+  if (action == "render" && !multi_devices.empty() &&
+      (from_row > 0 || from_col > 0 || (to_row >= 0 && to_row != (long long)opts.height) ||
+       (to_col >= 0 && to_col != (long long)opts.width)))
+    return usage("--gpus / --devices render whole frames (no --from-row/--from-col/--to-row/--to-col)");
+
   // The HIP runtime's start-up (driver and device enumeration) runs beside the scene load
   // below: the first HIP call of the process does it, wherever it is made.
   std::thread hip_init([] { (void)grt_device_count(); });
+  // on every way out of main from here: the start-up thread joined, then the multi-GPU
+  // frame's RCCL set-up waited for and torn down (a communicator still being created when
+  // the process exits brings the exit down)
   struct Joiner {
     std::thread& t;
+    bool multi;
     ~Joiner() {
       if (t.joinable()) t.join();
+      if (multi) grt_multi_release();
     }
-  } hip_init_join{hip_init};
+  } hip_init_join{hip_init, !multi_devices.empty()};
   // phase times of a render (printed on one [grt] line at the end; not in the reference)
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
@@ -519,8 +529,6 @@ int main(int argc, char** argv) {
                  opts.tone_mapping == GRT_TONE_GLOBAL_LINEAR ? "GlobalLinear" : "Reinhard");
   }
   const bool multi = !multi_devices.empty();
-  if (multi && (r0 != 0 || c0 != 0 || r1 != (uint32_t)opts.height || c1 != (uint32_t)opts.width))
-    return usage("--gpus / --devices render whole frames (no --from-row/--from-col/--to-row/--to-col)");
   if (supersampled)  // raytracer.rs:264-267
     std::fprintf(stderr, "[grt] INFO Rendering section from (%u, %u) to (%u, %u) with supersampling\n", r0, c0, r1,
                  c1);
@@ -623,9 +631,6 @@ int main(int argc, char** argv) {
     }
   }
   ph_write = ms_since(t_phase);
-  if (multi) grt_multi_release();
-  grt_scene_destroy(scene);
-  grt_host_scene_destroy(hs);
   std::fprintf(stderr, "[grt] INFO saved image to %s\n", filename.c_str());  // raytracer.rs:494
   // where the wall time went: TOML + texture decode + LUTs; the descriptor copy; the render
   // call (device upload on first use, trace, supersampling, D2H); tone map; encode + write
@@ -633,5 +638,9 @@ int main(int argc, char** argv) {
                "write %.1f, since start %.1f\n", ph_load, ph_create, ph_init, ph_render, ph_output, ph_write,
                ms_since(t_start));
   elapsed();
+  // teardown after the reference's measured span (main.rs:175-176 logs before its drops;
+  // the multi-GPU set-up is released by hip_init_join)
+  grt_scene_destroy(scene);
+  grt_host_scene_destroy(hs);
   return 0;
 }

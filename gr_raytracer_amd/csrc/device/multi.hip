@@ -20,6 +20,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -159,11 +160,35 @@ struct MultiDev {
 // One RCCL communicator per device of a device list (ncclCommInitAll), created on first
 // use and cached for the process: a frame after the first pays no setup.  `mu` serialises
 // frames on one device list (a communicator is driven by one thread at a time).
+// RCCL's start-up takes seconds (1.6-5.8 s for one device on the pool's boxes, most of it
+// loading its device code), and while it runs a kernel launch of the process can wait for
+// it; so the communicators are created on a thread of their own (`comm_ready`) started
+// once every device has enqueued its first frame's trace (note_launched), and a device
+// waits for them only before its first collective.
 struct MultiCtx {
   std::vector<int> devs;
   std::vector<ncclComm_t> comms;
   std::vector<MultiDev> d;
   std::mutex mu;
+  std::mutex cm;  // the three below
+  std::condition_variable cv;
+  int launched = 0;
+  bool started = false;
+  std::shared_future<std::string> comm_ready;  // "" once the communicators exist, else the error
+
+  // A device thread of the first frame has enqueued its trace (or failed before): the
+  // last of them starts the communicators' creation.
+  void note_launched() {
+    std::lock_guard<std::mutex> lk(cm);
+    if (started || ++launched < (int)devs.size()) return;
+    started = true;
+    MultiCtx* cp = this;
+    comm_ready = std::async(std::launch::async, [cp]() -> std::string {
+                   const ncclResult_t r = ncclCommInitAll(cp->comms.data(), (int)cp->devs.size(), cp->devs.data());
+                   return r == ncclSuccess ? std::string() : std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+                 }).share();
+    cv.notify_all();
+  }
 };
 std::mutex g_ctx_mu;
 std::vector<std::unique_ptr<MultiCtx>> g_ctx;
@@ -178,7 +203,6 @@ int get_ctx(const std::vector<int>& devs, MultiCtx** out) {
   auto c = std::make_unique<MultiCtx>();
   c->devs = devs;
   c->comms.resize(devs.size());
-  NCCL_TRY(ncclCommInitAll(c->comms.data(), (int)devs.size(), devs.data()));
   c->d.resize(devs.size());
   for (size_t i = 0; i < devs.size(); ++i) {
     MultiDev& m = c->d[i];
@@ -190,6 +214,34 @@ int get_ctx(const std::vector<int>& devs, MultiCtx** out) {
   *out = c.get();
   g_ctx.push_back(std::move(c));
   return 0;
+}
+
+// A device list: 1..GRT_MULTI_MAX_DEVICES distinct, valid ordinals.
+int check_devices(int n_devices, const int* devices, std::vector<int>* out) {
+  if (!devices) return fail(-EINVAL, "null argument");
+  if (n_devices < 1 || n_devices > grt::MULTI_MAX) return fail(-EINVAL, "n_devices must be in 1..GRT_MULTI_MAX_DEVICES");
+  std::vector<int> devs(devices, devices + n_devices);
+  for (int a = 0; a < n_devices; ++a)
+    for (int b = a + 1; b < n_devices; ++b)
+      if (devs[a] == devs[b]) return fail(-EINVAL, "a device appears twice (one RCCL rank per GPU)");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  for (int d : devs)
+    if (d < 0 || d >= ndev) return fail(-ENODEV, "invalid device ordinal");
+  *out = std::move(devs);
+  return 0;
+}
+
+// The communicators of C, waited for (created beside the first frame's traces).
+int comms_ready(MultiCtx& C) {
+  std::shared_future<std::string> f;
+  {
+    std::unique_lock<std::mutex> lk(C.cm);
+    C.cv.wait(lk, [&] { return C.started; });
+    f = C.comm_ready;
+  }
+  const std::string err = f.get();
+  return err.empty() ? 0 : fail(-EIO, err);
 }
 
 // A reusable barrier of the device threads.  arrive(ok) returns false on every thread
@@ -323,6 +375,7 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
   // arrives at the ones it has not reached with ok = false, below)
   const int n_barriers = P.super ? 2 : 1;
   int passed = 0;
+  bool noted = false;  // C.note_launched() called
   auto barrier = [&]() -> bool {
     ++passed;
     return bar.arrive(true);
@@ -361,6 +414,8 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
       int rc = grt_render_shard_async(scene, dev, st, &sh, x32, cls, status, x64, steps, stop, (uint64_t*)B.stats);
       if (rc) return rc;
     }
+    noted = true;
+    C.note_launched();
     if (P.super) {
       // (Y, alpha) and class of every local pixel, then ONE allgather: every device gets
       // the whole frame's neighbourhood records, de-interleaved into frame order
@@ -371,6 +426,7 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
         HIP_TRY(hipGetLastError());
       }
       HIP_TRY(hipStreamSynchronize(st));
+      if (int rc = comms_ready(C)) return rc;
       if (!barrier()) return fail(-ECANCELED, "another device failed");
       HIP_TRY(hipEventRecord(M.ev[2], st));
       NCCL_TRY(ncclAllGather(B.ag_send, B.ag_recv, P.ag_bytes, ncclUint8, C.comms[i], st));
@@ -428,6 +484,7 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
     HIP_TRY(hipStreamSynchronize(st));
     // ONE gather: every device sends its block to devices[0] (grouped send / receive;
     // devices[0] sends to itself too, so every frame takes the same RCCL path)
+    if (int rc = comms_ready(C)) return rc;
     if (!barrier()) return fail(-ECANCELED, "another device failed");
     HIP_TRY(hipEventRecord(M.ev[4], st));
     NCCL_TRY(ncclGroupStart());
@@ -469,6 +526,7 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
     return 0;
   };
   R.rc = run();
+  if (!noted) C.note_launched();  // failed before its trace: the others must not wait
   if (R.rc) {
     R.err = grt_last_error();
     // the barriers this thread has not reached: the other threads stop there instead of
@@ -490,16 +548,9 @@ int grt_render_frame_multi(grt_scene* scene, int n_devices, const int* devices, 
   if (n_supersampled) *n_supersampled = 0;
   if (failures) failures->count = 0;
   if (!scene || !devices || !out) return fail(-EINVAL, "null argument");
-  if (n_devices < 1 || n_devices > grt::MULTI_MAX) return fail(-EINVAL, "n_devices must be in 1..GRT_MULTI_MAX_DEVICES");
   if (band_rows == 0) return fail(-EINVAL, "band_rows must be >= 1");
-  std::vector<int> devs(devices, devices + n_devices);
-  for (int a = 0; a < n_devices; ++a)
-    for (int b = a + 1; b < n_devices; ++b)
-      if (devs[a] == devs[b]) return fail(-EINVAL, "a device appears twice (one RCCL rank per GPU)");
-  int ndev = 0;
-  HIP_TRY(hipGetDeviceCount(&ndev));
-  for (int d : devs)
-    if (d < 0 || d >= ndev) return fail(-ENODEV, "invalid device ordinal");
+  std::vector<int> devs;
+  if (int rc = check_devices(n_devices, devices, &devs)) return rc;
   Plan P;
   P.n_dev = (uint32_t)n_devices;
   P.band = band_rows;
@@ -625,6 +676,7 @@ void grt_multi_release(void) {
   std::lock_guard<std::mutex> lk(g_ctx_mu);
   for (auto& c : g_ctx) {
     std::lock_guard<std::mutex> l2(c->mu);
+    const bool have_comms = c->started && c->comm_ready.get().empty();
     for (auto& m : c->d) {
       (void)hipSetDevice(m.device);
       if (m.st) (void)hipStreamSynchronize(m.st);
@@ -633,7 +685,8 @@ void grt_multi_release(void) {
         if (e) (void)hipEventDestroy(e);
       if (m.st) (void)hipStreamDestroy(m.st);
     }
-    for (auto& cm : c->comms) (void)ncclCommDestroy(cm);
+    if (have_comms)
+      for (auto& cm : c->comms) (void)ncclCommDestroy(cm);
   }
   g_ctx.clear();
 }
