@@ -603,6 +603,15 @@ int grt_render_frame_multi(grt_scene* scene, int n_devices, const int* devices, 
                       std::ref(bar), std::ref(R[i]));
     device_part(scene, *C, P, 0, cfg, sampling_mask_xyza, out, failures, bar, R[0]);
     for (auto& t : th) t.join();
+    {  // no communicator is still being created when this call returns (a frame that
+       // failed before its collectives has not waited for them)
+      std::shared_future<std::string> f;
+      {
+        std::lock_guard<std::mutex> l2(C->cm);
+        if (C->started) f = C->comm_ready;
+      }
+      if (f.valid()) (void)f.get();
+    }
     for (uint32_t i = 0; i < P.n_dev; ++i)
       if (R[i].rc && R[i].rc != -ECANCELED) return fail(R[i].rc, "device " + std::to_string(devs[i]) + ": " + R[i].err);
     for (uint32_t i = 0; i < P.n_dev; ++i)
