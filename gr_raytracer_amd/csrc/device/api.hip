@@ -557,11 +557,20 @@ bool schedule_wanted(const grt_scene* s, const grt::WorkList& wl, const Knobs& k
   return (g == GRT_GEOM_KERR || g == GRT_GEOM_SCHWARZSCHILD) && s->desc.max_steps >= 8ull * PROBE_CAP &&
          tiles >= 1024;
 }
+// Schwarzschild frames the probe pass is not worth (automatic mode): the tile order from
+// each tile's impact parameter instead (impact_key_kernel; no integration, ~0.1 ms).  C2
+// one frame alone 1,280-1,282 -> 1,263-1,271 ms; two frames in flight unchanged
+// (1,234-1,241 against 1,240 ms), and with the two-ended queue slower (1,253 ms); frames
+// identical (profiles/r06x).
+bool impact_wanted(const grt_scene* s, const grt::WorkList& wl, const Knobs& k) {
+  return !wl.pixel_index && k.schedule == -1 && s->desc.geometry == GRT_GEOM_SCHWARZSCHILD &&
+         wl.n_items / 64 >= 1024 && !schedule_wanted(s, wl, k);
+}
 
 // Enqueue the probe pass and the sort; returns the device tile order in *order.
 // quad: the Kerr-Schild probe on quads, -1 automatic, 0 never, 1 always (grt_debug_probe_keys).
 int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hipStream_t stream,
-                       const uint32_t** order, int quad_mode = -1) {
+                       const uint32_t** order, int quad_mode = -1, bool impact = false) {
   const uint32_t tiles_x = wl.tiles_x, tiles_y = (uint32_t)(wl.n_items / 64 / wl.tiles_x);
   const uint64_t n = (uint64_t)tiles_x * tiles_y;
   size_t temp_bytes = 0;
@@ -591,6 +600,13 @@ int enqueue_tile_order(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl, hi
   uint32_t* idx = (uint32_t*)take(n * 4);
   uint32_t* ord = (uint32_t*)take(n * 4);
   void* temp = take(temp_bytes);
+  if (impact) {  // predicted lengths, no probe rays; no key counts as capped
+    HIP_TRY(grt::launch_impact_keys(dc.d_scene, wl, (uint32_t)n, probe, stream));
+    HIP_TRY(grt::launch_tile_order(probe, tiles_x, tiles_y, 0xffffffffu, keys, keys_sorted, idx, ord, temp, &temp_bytes,
+                                   stream));
+    *order = ord;
+    return 0;
+  }
   const uint32_t cap = probe_cap(s);
   // Kerr-Schild probe rays on quads when they fill at most 2 waves per SIMD that way
   // (probe_quad_kernel: a C4 1/8 shard's 32,768 probes); above that the one-lane probe,
@@ -674,6 +690,9 @@ int enqueue_trace(grt_scene* s, DeviceCopy& dc, const grt::WorkList& wl_in, cons
     if (rc0) return rc0;
     // longest tiles to the priority wave of each SIMD, shortest to the others (WorkList)
     wl.two_ended = (k.two_ended != 0 && wl.n_items < (1ull << 31)) ? 1u : 0u;
+  } else if (impact_wanted(s, wl, k)) {
+    int rc0 = enqueue_tile_order(s, dc, wl, stream, &wl.tile_order, -1, true);
+    if (rc0) return rc0;
   }
   HIP_TRY(hipMemsetAsync(dc.d_counter, 0, sizeof(unsigned long long), stream));
   if (dc.vol) {  // jobs, cursor; the march passes' cursors
@@ -880,10 +899,12 @@ int grt_debug_ray_times(grt_scene* scene, int device, uint64_t* out, uint64_t n,
 #endif
 
 // Test hook (not in grt_api.h): the probe keys (probe_kernel / probe_quad_kernel) of a
-// row-band shard with the probe forced onto quads (quad = 1) or onto one lane per ray (0).
+// row-band shard with the probe forced onto quads (quad = 1) or onto one lane per ray (0),
+// or the Schwarzschild impact-parameter keys (quad = 2, impact_key_kernel).
 int grt_debug_probe_keys(grt_scene* s, int device, const grt_row_shard* sh, int quad, uint32_t* keys_out,
                          uint64_t n_tiles) {
-  if (!s || !sh || !keys_out || (quad != 0 && quad != 1)) return fail(-EINVAL, "probe keys: bad argument");
+  if (!s || !sh || !keys_out || quad < 0 || quad > 2) return fail(-EINVAL, "probe keys: bad argument");
+  if (quad == 2 && s->desc.geometry != GRT_GEOM_SCHWARZSCHILD) return fail(-EINVAL, "impact keys: Schwarzschild only");
   DeviceCopy* dc;
   int rc;
   if ((rc = ensure_device(s, device, &dc))) return rc;
@@ -896,7 +917,7 @@ int grt_debug_probe_keys(grt_scene* s, int device, const grt_row_shard* sh, int 
   wl.n_shards = sh->n_shards;
   if (wl.n_items / 64 != n_tiles || wl.n_items % 64 != 0) return fail(-EINVAL, "tile count differs");
   const uint32_t* order = nullptr;
-  if ((rc = enqueue_tile_order(s, *dc, wl, nullptr, &order, quad))) return rc;
+  if ((rc = enqueue_tile_order(s, *dc, wl, nullptr, &order, quad == 2 ? -1 : quad, quad == 2))) return rc;
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(keys_out, dc->sched_mem, n_tiles * 4, hipMemcpyDeviceToHost));
   return 0;

@@ -2886,6 +2886,42 @@ __global__ void __launch_bounds__(64) probe_kernel(const DevScene* __restrict__ 
   steps_out[t] = key;
 }
 
+// Work-order key of a Schwarzschild tile without integrating: the predicted steps of its
+// probe pixel's ray from the impact parameter b = L / E of its initial momentum (E =
+// (1 - r_s / r) dt/dl, L = r^2 sqrt((dtheta/dl)^2 + sin^2 theta (dphi/dl)^2)).  A ray with
+// b above the photon orbit's b_c = (3 sqrt 3 / 2) r_s escapes to the celestial sphere
+// (~max_radius unit steps), one below it falls in (a few hundred steps), and near b_c
+// both wind round the photon sphere for ~ln(1 / |b / b_c - 1|) more turns.  Only the
+// queue order depends on it, never a result.
+__global__ void __launch_bounds__(64) impact_key_kernel(const DevScene* __restrict__ Sp, WorkList wl,
+                                                        uint32_t n_tiles, uint32_t* __restrict__ keys_out) {
+  const DevScene& S = *Sp;
+  glibc::tables_to_lds();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles) return;
+  const uint32_t tr = t / wl.tiles_x, tc = t % wl.tiles_x;
+  const uint32_t r = min(tr * 8 + 3, wl.rows - 1), c = min(tc * 8 + 3, wl.cols - 1);
+  double y[8];
+  RayConst rc;
+  init_ray<GRT_GEOM_SCHWARZSCHILD>(S, (double)(wl.row0 + shard_frame_row(wl.band_rows, wl.shard, wl.n_shards, r)),
+                                   (double)(wl.col0 + c), y, rc);
+  const double rs = S.radius, rr = y[1], sn = sin(y[2]);
+  const double e = fabs((1.0 - rs / rr) * y[4]);
+  const double l = rr * rr * sqrt(y[6] * y[6] + sn * sn * y[7] * y[7]);
+  const double bc = 2.598076211353316 * rs;
+  const double b = l / e;
+  const double x = fmax(fabs(b - bc) / bc, 1e-12);
+  const double len = (b > bc ? sqrt(S.max_radius_sq) : 300.0) + 700.0 * fmax(0.0, -log(x));
+  keys_out[t] = (len > 0.0 && len < 4.0e9) ? (uint32_t)len : (len >= 4.0e9 ? 4000000000u : 0u);  // NaN: 0
+}
+
+hipError_t launch_impact_keys(const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t* d_keys,
+                              hipStream_t stream) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(impact_key_kernel, dim3((n_tiles + 63) / 64), dim3(64), 0, stream, d_scene, wl, n_tiles, d_keys);
+  return hipGetLastError();
+}
+
 // probe_kernel<KERR> with each probe ray on the 4 lanes of a quad (rhs_ks_quad, as in
 // tail_kernel): the same operations on the same values, so the same keys (GPU test
 // tests/test_gpu_schedule.py).  For a pass of few probe rays (a 1/8 row-band shard of

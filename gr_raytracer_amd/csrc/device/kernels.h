@@ -26,6 +26,10 @@ constexpr int TAIL_RAYS_PER_BLOCK = 256 / 4;
 // quad (Kerr-Schild only): each probe ray on a quad of lanes (probe_quad_kernel), same keys.
 hipError_t launch_probe(int geometry, const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t cap,
                         uint32_t* d_steps, bool quad, hipStream_t stream);
+// Schwarzschild work-order keys without a probe pass: predicted steps per 8x8 tile of
+// `wl` from the impact parameter of the tile's probe pixel (impact_key_kernel).
+hipError_t launch_impact_keys(const DevScene* d_scene, const WorkList& wl, uint32_t n_tiles, uint32_t* d_keys,
+                              hipStream_t stream);
 // Tile queue order from the probe keys (schedule.hip): 3x3-dilated keys (edge tiles of a
 // region of probes that reached `cap` boosted), sorted descending (stable).  `temp` /
 // `temp_bytes`: scratch, query with temp == NULL.

@@ -86,3 +86,41 @@ def test_probe_keys_schwarzschild_escaping_probes_finish_below_the_cap(grt, gpu)
     escaping = (k > 0.3 * 15000) & (k < cap)
     assert escaping.sum() > len(k) // 2  # most of the frame sees the celestial sphere
     assert np.median(k[escaping]) > 0.6 * 15000  # they ran out to max_radius, uncapped
+
+
+@pytest.mark.gpu
+def test_impact_keys_predict_escape_and_capture(grt, gpu):
+    """Schwarzschild frames without the probe pass (max-steps below 8 x the probe cap) take
+    their tile order from each tile's impact parameter (impact_key_kernel): the sky tiles
+    of C2's camera are predicted at least max_radius steps (escaping), the tiles at the
+    middle of the shadow a few hundred (captured), and the tiles at the photon ring's edge
+    the longest."""
+    from conftest import c2_opts
+
+    mr = 1000.0
+    opts = c2_opts(grt, width=256, height=256, max_radius=mr)
+    k = _probe_keys(grt, "schwarzschild.toml", opts, (0, 1), 2).reshape(32, 32)
+    assert (k[0, :] >= mr).all() and (k[:, 0] >= mr).all()  # frame border: sky
+    assert k[15:17, 15:17].max() < mr  # centre of the shadow
+    assert k.max() > mr + 700  # near-critical rays wind round the photon sphere
+
+
+@pytest.mark.gpu
+def test_impact_order_is_result_neutral(grt, gpu):
+    """The impact-parameter order (automatic mode) against row-major tiles: identical frames."""
+    from conftest import c2_opts
+    from gr_raytracer_amd import _lib as L
+
+    hs = host_scene(grt, "schwarzschild.toml", c2_opts(grt, width=256, height=256))
+    sc = grt.Scene(hs.desc_ptr(), keepalive=hs)
+    try:
+        out = {}
+        for mode in (-1, 0):
+            L.check(L.lib().grt_set_schedule(mode))
+            out[mode] = sc.render_pixels(device=gpu)
+    finally:
+        L.lib().grt_set_schedule(-1)
+    a, b = out[-1], out[0]
+    assert np.array_equal(a.xyza64, b.xyza64) and np.array_equal(a.ray_class, b.ray_class)
+    assert np.array_equal(a.steps, b.steps) and np.array_equal(a.stop_reason, b.stop_reason)
+    assert np.array_equal(a.status, b.status) and np.array_equal(a.hits, b.hits)
