@@ -91,3 +91,19 @@ def test_library_from_other_sources_is_refused(grt, tmp_path):
     r = subprocess.run([sys.executable, "-c", code, str(ROOT)], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 3, r.stdout + r.stderr
     assert "built from other sources" in r.stdout
+
+
+def test_kernel_symbols_cover_every_unit(grt):
+    """The kernel-symbol and code-hash helpers (PMC summaries record a kernel's own code
+    hash) read every translation unit's gfx950 code object: the main unit's kernels and
+    the KerrBL unit's (geodesic_kerr_bl.hip, namespace grt::kerr_bl)."""
+    from gr_raytracer_amd import _lib as L
+
+    syms = L.kernel_symbols()
+    assert any(s.startswith("_ZN3grt16integrate_kernelILi1ELb0EE") for s in syms)
+    assert any(s.startswith("_ZN3grt7kerr_bl16integrate_kernelILi3ELb0EE") for s in syms)
+    assert not any(s.startswith("_ZN3grt16integrate_kernelILi3ELb0EE") for s in syms)  # KerrBL left the main unit
+    main = L.kernel_symbol("grt::integrate_kernel<1, false>")
+    bl = L.kernel_symbol("grt::kerr_bl::integrate_kernel<3, false>")
+    assert main != bl and len(L.kernel_code_sha256(main)) == 64 and len(L.kernel_code_sha256(bl)) == 64
+    assert L.kernel_code_sha256(main) != L.kernel_code_sha256(bl)
