@@ -12,6 +12,7 @@
 // raytracer.rs:195-244, called from main.rs:80-116 via Raytracer::render_section
 // :460-497); every pixel here is identical to grt_render_pixels / grt_render_section of
 // the same frame on one device (tests/test_multi.py).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -25,6 +26,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "grt_api.h"
@@ -123,6 +125,47 @@ int fail(int code, const std::string& msg) {
   grt_host::set_error(msg);
   return code;
 }
+
+// RCCL is bound at the first multi-GPU frame (dlopen of librccl.so.1), not linked: a
+// process that never renders over several GPUs (the single-GPU CLI, the Python host) does
+// not load the 570 MB library at start-up, and libgrt.so loads where RCCL is absent.
+struct Rccl {
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclSend) Send = nullptr;
+  decltype(&ncclRecv) Recv = nullptr;
+  std::string error;  // why binding failed, or empty
+};
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      x.error = std::string("cannot load librccl.so.1: ") + (e ? e : "unknown error");
+      return x;
+    }
+    auto get = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn && x.error.empty()) x.error = std::string("librccl.so.1 has no ") + name;
+    };
+    get(x.CommInitAll, "ncclCommInitAll");
+    get(x.CommDestroy, "ncclCommDestroy");
+    get(x.GetErrorString, "ncclGetErrorString");
+    get(x.AllGather, "ncclAllGather");
+    get(x.GroupStart, "ncclGroupStart");
+    get(x.GroupEnd, "ncclGroupEnd");
+    get(x.Send, "ncclSend");
+    get(x.Recv, "ncclRecv");
+    return x;
+  }();
+  return r;
+}
 #define HIP_TRY(expr)                                                                    \
   do {                                                                                   \
     hipError_t _e = (expr);                                                              \
@@ -134,7 +177,7 @@ int fail(int code, const std::string& msg) {
 #define NCCL_TRY(expr)                                                                   \
   do {                                                                                   \
     ncclResult_t _r = (expr);                                                            \
-    if (_r != ncclSuccess) return fail(-EIO, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    if (_r != ncclSuccess) return fail(-EIO, std::string(#expr) + ": " + rccl().GetErrorString(_r)); \
   } while (0)
 
 constexpr uint64_t align256(uint64_t b) { return (b + 255) & ~255ull; }
@@ -184,8 +227,10 @@ struct MultiCtx {
     started = true;
     MultiCtx* cp = this;
     comm_ready = std::async(std::launch::async, [cp]() -> std::string {
-                   const ncclResult_t r = ncclCommInitAll(cp->comms.data(), (int)cp->devs.size(), cp->devs.data());
-                   return r == ncclSuccess ? std::string() : std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+                   const Rccl& R = rccl();
+                   if (!R.error.empty()) return R.error;
+                   const ncclResult_t r = R.CommInitAll(cp->comms.data(), (int)cp->devs.size(), cp->devs.data());
+                   return r == ncclSuccess ? std::string() : std::string("ncclCommInitAll: ") + R.GetErrorString(r);
                  }).share();
     cv.notify_all();
   }
@@ -429,7 +474,7 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
       if (int rc = comms_ready(C)) return rc;
       if (!barrier()) return fail(-ECANCELED, "another device failed");
       HIP_TRY(hipEventRecord(M.ev[2], st));
-      NCCL_TRY(ncclAllGather(B.ag_send, B.ag_recv, P.ag_bytes, ncclUint8, C.comms[i], st));
+      NCCL_TRY(rccl().AllGather(B.ag_send, B.ag_recv, P.ag_bytes, ncclUint8, C.comms[i], st));
       grt::GatherLayout L;
       std::memset(&L, 0, sizeof(L));
       L.cols = P.cols;
@@ -487,12 +532,12 @@ void device_part(grt_scene* scene, MultiCtx& C, const Plan& P, int i, const grt_
     if (int rc = comms_ready(C)) return rc;
     if (!barrier()) return fail(-ECANCELED, "another device failed");
     HIP_TRY(hipEventRecord(M.ev[4], st));
-    NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(B.block, P.block[i], ncclUint8, 0, C.comms[i], st));
+    NCCL_TRY(rccl().GroupStart());
+    NCCL_TRY(rccl().Send(B.block, P.block[i], ncclUint8, 0, C.comms[i], st));
     if (i == 0)
       for (uint32_t s = 0; s < P.n_dev; ++s)
-        NCCL_TRY(ncclRecv(B.gathered + P.block_off[s], P.block[s], ncclUint8, (int)s, C.comms[i], st));
-    NCCL_TRY(ncclGroupEnd());
+        NCCL_TRY(rccl().Recv(B.gathered + P.block_off[s], P.block[s], ncclUint8, (int)s, C.comms[i], st));
+    NCCL_TRY(rccl().GroupEnd());
     if (i == 0) {
       const grt::GatherLayout L = gather_layout(P);
       grt::GatherDst d{};
@@ -695,7 +740,7 @@ void grt_multi_release(void) {
       if (m.st) (void)hipStreamDestroy(m.st);
     }
     if (have_comms)
-      for (auto& cm : c->comms) (void)ncclCommDestroy(cm);
+      for (auto& cm : c->comms) (void)rccl().CommDestroy(cm);
   }
   g_ctx.clear();
 }
